@@ -1,0 +1,295 @@
+/*
+ * rrte_hip.h — C ABI of the MI355X-native replacement for rrte-renderer's
+ * per-pixel ray->scene loop.
+ *
+ * Replaces (reference paths relative to Melthizar/RRTE @ 2025-06-14):
+ *   Raytracer::new / update_config / render
+ *       crates/rrte-renderer/src/raytracer.rs:35-51 (render 45-89, ray_color 92-148)
+ *   SceneObject::intersect for Sphere/Plane/Triangle/Cube/Cylinder/Cone/Capsule
+ *       crates/rrte-renderer/src/primitives.rs:6-18, 57-725
+ *   Light::illuminate (PointLight / Directional / Spot / Ambient)
+ *       crates/rrte-renderer/src/light.rs:5-26, 87-121, 182-194, 288-338, 364-397
+ *   Material::albedo / ambient_color
+ *       crates/rrte-renderer/src/material.rs:5-19, 55-81
+ *   Camera::generate_ray   crates/rrte-renderer/src/camera.rs:98-133
+ *   SDF / CSGOperation / Deformer (README-only in the reference:
+ *       README.md:458-510; build-defined here)
+ *
+ * Conventions
+ *   - Plain C, POD structs, caller owns every buffer it passes in.
+ *   - A context owns device memory and its HIP stream; one context per
+ *     host thread (not internally synchronised).  Multi-GPU composition is
+ *     internal to a context once rrte_hip_comm_init has been called.
+ *   - No exceptions, panics or aborts cross this ABI: every entry point
+ *     returns an rrte_status; rrte_hip_last_error() has the message.
+ *   - Output images are RGBA8, row-major, row 0 = top of the image
+ *     (v = 0 -> ndc_y = +1, camera.rs:101), exactly the layout of the
+ *     Vec<u8> returned by Raytracer::render (raytracer.rs:54-88).
+ */
+#ifndef RRTE_HIP_H
+#define RRTE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RRTE_ABI_VERSION 1u
+
+/* ------------------------------------------------------------------ status */
+typedef enum rrte_status {
+    RRTE_OK = 0,
+    RRTE_INVALID_ARG = 1,      /* null pointer, zero size, malformed SDF program, ... */
+    RRTE_HIP_ERROR = 2,        /* any HIP runtime failure (message in last_error)     */
+    RRTE_RCCL_ERROR = 3,       /* RCCL failure during multi-GPU composition            */
+    RRTE_UNSUPPORTED_PRIM = 4, /* unknown prim kind / light kind / SDF op              */
+    RRTE_NO_DEVICE = 5         /* no HIP device visible / device index out of range    */
+} rrte_status;
+
+/* --------------------------------------------------------------- prim kinds */
+typedef enum rrte_prim_kind {
+    RRTE_PRIM_SPHERE = 0,   /* primitives.rs:57-81   p: center[0..2], radius[3]            */
+    RRTE_PRIM_PLANE = 1,    /* primitives.rs:133-149 p: point[0..2], unit normal[4..6]     */
+    RRTE_PRIM_TRIANGLE = 2, /* primitives.rs:208-244 p: v0,v1,v2 [0..8], n0,n1,n2 [9..17]  */
+    RRTE_PRIM_CUBE = 3,     /* primitives.rs:301-364 p: center[0..2], size[4..6] (full)    */
+    RRTE_PRIM_CYLINDER = 4, /* primitives.rs:419-465 p: center[0..2], radius[3], height[4] */
+    RRTE_PRIM_CONE = 5,     /* primitives.rs:520-571 p: center[0..2], radius[3], height[4] */
+    RRTE_PRIM_CAPSULE = 6,  /* primitives.rs:626-725 p: center[0..2], radius[3], height[4] */
+    RRTE_PRIM_SDF = 7       /* build-defined SDFObject: sphere-traced node program;
+                               p: bounding sphere center[0..2], radius[3]                 */
+} rrte_prim_kind;
+
+/* One SceneObject lowered to POD (192 bytes).  trs is the object's
+ * rrte_math::Transform {position, rotation quat (x,y,z,w), scale}
+ * (transform.rs:6-10); Cube/Cylinder/Cone/Capsule apply it exactly as the
+ * reference does (local ray through inverse_matrix, hit back through
+ * to_matrix); Sphere/Plane/Triangle ignore it, as the reference does. */
+typedef struct rrte_prim {
+    uint32_t kind;           /* rrte_prim_kind                                      */
+    int32_t material;        /* index into rrte_scene_ir.materials; -1 = none
+                                (ray_color returns BLACK, raytracer.rs:139-143)     */
+    uint32_t sdf_first;      /* SDF: index of this object's first node             */
+    uint32_t sdf_count;      /* SDF: number of nodes in its postfix program        */
+    uint32_t sdf_max_steps;  /* SDF: sphere-tracing step cap                        */
+    float sdf_step_scale;    /* SDF: step multiplier (<1 for non-Lipschitz deformers) */
+    float sdf_hit_eps;       /* SDF: relative hit epsilon: hit when d < eps * t     */
+    uint32_t flags;          /* reserved, 0                                         */
+    float p[20];             /* geometry, per kind (see rrte_prim_kind)             */
+    float trs[10];           /* position[3], rotation quat xyzw[4], scale[3]        */
+    float _pad[10];
+} rrte_prim;
+
+/* ----------------------------------------------------------------- materials */
+typedef enum rrte_material_kind {
+    RRTE_MAT_LAMBERTIAN = 0, /* material.rs:45-81   */
+    RRTE_MAT_METAL = 1,      /* material.rs:85-120  */
+    RRTE_MAT_DIELECTRIC = 2, /* material.rs:124-183 */
+    RRTE_MAT_EMISSIVE = 3    /* material.rs:187-213 */
+} rrte_material_kind;
+
+typedef struct rrte_material {
+    uint32_t kind;       /* rrte_material_kind                               */
+    float fuzz;          /* metal roughness                                  */
+    float ior;           /* dielectric index of refraction                   */
+    float _pad0;
+    float albedo[4];     /* Material::albedo() as rrte_math::Color (r,g,b,a) */
+} rrte_material;         /* 32 bytes */
+
+/* -------------------------------------------------------------------- lights */
+typedef enum rrte_light_kind {
+    RRTE_LIGHT_POINT = 0,       /* light.rs:123-220 */
+    RRTE_LIGHT_DIRECTIONAL = 1, /* light.rs:57-121  */
+    RRTE_LIGHT_SPOT = 2,        /* light.rs:222-338 */
+    RRTE_LIGHT_AMBIENT = 3      /* light.rs:340-397 */
+} rrte_light_kind;
+
+typedef struct rrte_light {
+    uint32_t kind;        /* rrte_light_kind                                   */
+    float intensity;
+    float range;          /* PointLight/SpotLight (default 100, light.rs:142)  */
+    float linear;         /* linear_attenuation   (default 0.09)               */
+    float quadratic;      /* quadratic_attenuation (default 0.032)             */
+    float inner_angle;    /* SpotLight, radians                                */
+    float outer_angle;    /* SpotLight, radians                                */
+    float _pad0;
+    float position[4];    /* xyz, w unused                                     */
+    float direction[4];   /* Directional/Spot unit direction xyz               */
+    float color[4];       /* rrte_math::Color (r,g,b,a)                        */
+} rrte_light;             /* 80 bytes */
+
+/* ---------------------------------------------------------- SDF node program */
+/* An SDFObject's tree is flattened to postfix order.  Leaves push a distance
+ * evaluated at the current point; CSG ops pop b, pop a, push op(a, b);
+ * deformers save the current point and replace it with deform(point);
+ * POP_POINT restores the saved point.  A Deformer chain d1.chain(d2)
+ * (README.md:496-502) is emitted as d1, d2, <subtree>, POP_POINT, POP_POINT.
+ * Value stack <= RRTE_SDF_MAX_STACK, point stack <= RRTE_SDF_MAX_POINT_STACK.
+ * Formulas: DESIGN.md §SDF (build-defined; the reference has no SDF code). */
+typedef enum rrte_sdf_op {
+    RRTE_SDF_SPHERE = 1,    /* f: center[0..2], radius[3]                     */
+    RRTE_SDF_BOX = 2,       /* f: center[0..2], size[4..6] (full extents)     */
+    RRTE_SDF_CYLINDER = 3,  /* f: center, radius[3], height[4]  (Y axis)      */
+    RRTE_SDF_PRISM = 4,     /* f: center, size[4..6] (triangle in XY, depth Z)*/
+    RRTE_SDF_TORUS = 5,     /* f: center, major[3], minor[4]   (XZ plane)     */
+    RRTE_SDF_TUBE = 6,      /* f: center, outer[3], inner[4], height[5]       */
+    RRTE_SDF_RING = 7,      /* f: center, major[3], minor[4]   (XY plane)     */
+    RRTE_SDF_CONE = 8,      /* f: center, radius[3], height[4] (apex +Y)      */
+    RRTE_SDF_CAPSULE = 9,   /* f: center, radius[3], height[4] (Y axis)       */
+    RRTE_SDF_ELLIPSOID = 10,/* f: center, radii[4..6]                         */
+
+    RRTE_SDF_UNION = 32,
+    RRTE_SDF_DIFFERENCE = 33,
+    RRTE_SDF_INTERSECTION = 34,
+    RRTE_SDF_SMOOTH_UNION = 35,        /* f[0] = k */
+    RRTE_SDF_SMOOTH_DIFFERENCE = 36,   /* f[0] = k */
+    RRTE_SDF_SMOOTH_INTERSECTION = 37, /* f[0] = k */
+
+    RRTE_SDF_BEND = 64,  /* f: pivot[0..2], amount[3]; i: plane-normal axis[0], driving axis[1] */
+    RRTE_SDF_TWIST = 65, /* f: pivot[0..2], rate[3];   i: axis[0]                            */
+    RRTE_SDF_TAPER = 66, /* f: pivot[0..2], start[3], end[4], length[5]; i: axis[0]          */
+    RRTE_SDF_NOISE = 67, /* f: pivot[0..2], frequency[3], amplitude[4], persistence[5];
+                            i: octaves[0], seed[1]                                         */
+    RRTE_SDF_WAVE = 68,  /* f: pivot[0..2], amplitude[3], frequency[4]; i: axis[0], displaced axis[1] */
+
+    RRTE_SDF_POP_POINT = 96
+} rrte_sdf_op;
+
+#define RRTE_SDF_MAX_STACK 8
+#define RRTE_SDF_MAX_POINT_STACK 4
+#define RRTE_SDF_MAX_OCTAVES 8
+
+typedef struct rrte_sdf_node {
+    uint32_t op;      /* rrte_sdf_op */
+    uint32_t i[3];    /* integer args (axes 0=X 1=Y 2=Z, octaves, seed) */
+    float f[12];      /* float args */
+} rrte_sdf_node;      /* 64 bytes */
+
+/* -------------------------------------------------------------------- camera */
+typedef enum rrte_projection { RRTE_PERSPECTIVE = 0, RRTE_ORTHOGRAPHIC = 1 } rrte_projection;
+
+/* rrte_renderer::Camera (camera.rs:24-31): transform + projection. */
+typedef struct rrte_camera {
+    float position[3];
+    uint32_t projection;   /* rrte_projection */
+    float rotation[4];     /* quat x,y,z,w (Camera::look_at, camera.rs:85-95) */
+    float scale[3];
+    float fov;             /* radians */
+    float aspect_ratio;
+    float near_plane;
+    float far_plane;
+    float left, right, bottom, top; /* orthographic */
+    float _pad[1];
+} rrte_camera;             /* 80 bytes */
+
+/* ------------------------------------------------------------ render params */
+typedef enum rrte_mode {
+    /* Reference formula (raytracer.rs:92-148): ambient albedo*0.01 + sum of
+     * light.color*intensity*attenuation (no N.L, no shadows) + albedo *
+     * ray_color(scatter, depth-1). */
+    RRTE_MODE_REFCOMPAT = 0,
+    /* north_star Lambert/shadow pass: ambient albedo*0.01 + sum over lights of
+     * albedo * color*intensity * att * max(0, N.L) * visibility(shadow ray). */
+    RRTE_MODE_LAMBERT_SHADOW = 1
+} rrte_mode;
+
+typedef enum rrte_jitter {
+    RRTE_JITTER_CENTER = 0, /* xi = 0.5: deterministic parity config           */
+    RRTE_JITTER_RANDOM = 1  /* counter-based RNG keyed by (seed, pixel, sample) */
+} rrte_jitter;
+
+#define RRTE_FLAG_F32_LINEAR 1u  /* f32 output holds the averaged linear colour (pre-gamma, unclamped) */
+
+typedef struct rrte_render_params {
+    uint32_t width, height;
+    uint32_t samples_per_pixel; /* RaytracerConfig::samples_per_pixel */
+    uint32_t max_depth;         /* RaytracerConfig::max_depth         */
+    uint32_t mode;              /* rrte_mode                          */
+    uint32_t jitter;            /* rrte_jitter                        */
+    uint32_t seed;
+    uint32_t flags;             /* RRTE_FLAG_*                        */
+    float background[4];        /* RaytracerConfig::background_color  */
+    float t_min;                /* closest-hit lower bound (raytracer.rs:107: 0.001) */
+    float shadow_bias;          /* LAMBERT_SHADOW: origin offset along N and t_min    */
+    float gamma;                /* 2.2 (raytracer.rs:79)              */
+    uint32_t band_rows;         /* multi-GPU interleave: rows per band (0 = whole image) */
+} rrte_render_params;           /* 64 bytes */
+
+/* ---------------------------------------------------------------- scene IR */
+typedef struct rrte_scene_ir {
+    const rrte_prim* prims;         uint32_t num_prims;
+    const rrte_material* materials; uint32_t num_materials;
+    const rrte_light* lights;       uint32_t num_lights;
+    const rrte_sdf_node* sdf_nodes; uint32_t num_sdf_nodes;
+    rrte_camera camera;
+} rrte_scene_ir;
+
+typedef struct rrte_stats {
+    uint64_t primary_rays;   /* W*H*spp of the last frame (this rank's rows)   */
+    uint64_t shadow_rays;    /* shadow rays actually cast in the last frame    */
+    double kernel_ms;        /* ray kernel time of the last frame (HIP events) */
+    double gather_ms;        /* RCCL gather + de-interleave time               */
+    double upload_ms;        /* scene H2D time (0 when the scene was cached)   */
+    uint64_t frames;         /* frames rendered by this context                */
+} rrte_stats;
+
+typedef struct rrte_ctx rrte_ctx;
+
+/* ------------------------------------------------------------- entry points */
+uint32_t rrte_hip_abi_version(void);
+
+/* Create a context on HIP device `device` (>= 0). */
+rrte_status rrte_hip_create(int device, rrte_ctx** out);
+void rrte_hip_destroy(rrte_ctx* ctx);
+const char* rrte_hip_last_error(const rrte_ctx* ctx);
+
+/* Raytracer::render: blocking; writes W*H*4 bytes to host `out_rgba8`. */
+rrte_status rrte_hip_render(rrte_ctx* ctx, const rrte_scene_ir* scene,
+                            const rrte_render_params* params, uint8_t* out_rgba8);
+
+/* Parity variant: also writes W*H*4 floats (post-gamma, post-clamp, pre-
+ * quantisation; or linear if RRTE_FLAG_F32_LINEAR).  Either pointer may be null. */
+rrte_status rrte_hip_render_f32(rrte_ctx* ctx, const rrte_scene_ir* scene,
+                                const rrte_render_params* params, uint8_t* out_rgba8,
+                                float* out_rgba32f);
+
+/* Device-resident variant for throughput measurement and display: enqueue
+ * one frame on `stream` (a hipStream_t, or null for the context's stream)
+ * writing to device buffers (either may be null).  Returns without
+ * synchronising; shadow-ray counts accumulate on the device and are folded
+ * into rrte_hip_stats at the next synchronising call. */
+rrte_status rrte_hip_render_async(rrte_ctx* ctx, const rrte_scene_ir* scene,
+                                  const rrte_render_params* params, void* d_out_rgba8,
+                                  void* d_out_rgba32f, void* stream);
+rrte_status rrte_hip_synchronize(rrte_ctx* ctx);
+
+rrte_status rrte_hip_stats(rrte_ctx* ctx, rrte_stats* out);
+
+/* ----------------------------------------------------- multi-GPU (RCCL/xGMI) */
+/* Row-band partition: band b (band_rows rows) belongs to rank b % nranks.
+ * rrte_hip_render_gather renders this rank's bands and gathers every rank's
+ * bands to `root`, which de-interleaves them into the full image. */
+#define RRTE_UNIQUE_ID_BYTES 128
+rrte_status rrte_hip_comm_unique_id(uint8_t out_id[RRTE_UNIQUE_ID_BYTES]);
+rrte_status rrte_hip_comm_init(rrte_ctx* ctx, int nranks, int rank,
+                               const uint8_t id[RRTE_UNIQUE_ID_BYTES]);
+/* Blocking: on the root writes the full W*H*4 image to host out_rgba8 (may be
+ * null to keep it on the device); non-root ranks ignore out_rgba8. */
+rrte_status rrte_hip_render_gather(rrte_ctx* ctx, const rrte_scene_ir* scene,
+                                   const rrte_render_params* params, int root,
+                                   uint8_t* out_rgba8);
+/* Async device variant: d_full_rgba8 (root only, W*H*4 bytes) receives the frame. */
+rrte_status rrte_hip_render_gather_async(rrte_ctx* ctx, const rrte_scene_ir* scene,
+                                         const rrte_render_params* params, int root,
+                                         void* d_full_rgba8, void* stream);
+
+/* Host-side helpers exported for the bindings (no device work). */
+/* Rows owned by `rank` under band interleave, in the order they are packed. */
+uint32_t rrte_hip_band_rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RRTE_HIP_H */

@@ -1,0 +1,66 @@
+/*
+ * rrte_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's per-pixel ray->scene loop
+ * (Melthizar/RRTE crates/rrte-renderer/src/raytracer.rs:45-148 and the
+ * functions it calls).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the
+ * CPU baseline — never as the product path.
+ *
+ * Parity status:
+ *   - The reference is Rust; no cargo/rustc exists in this image and the
+ *     reference ships no tests, fixtures or golden vectors (SURVEY.md §4,
+ *     §8c).  The restatement is therefore pinned only by hand-derived
+ *     known-answer tests written from the reference source and by an
+ *     independent numpy restatement (tests/): "parity unpinned" against
+ *     the Rust binary itself.
+ *   - glam 0.24.2 arithmetic (Vec3 normalize/dot/cross, Quat::from_rotation_arc,
+ *     Quat*Vec3, Mat4 SRT + inverse) is restated from glam's published
+ *     algorithms; unpinned.
+ *   - SDF / CSG / deformers / LAMBERT_SHADOW are build-defined (README-only
+ *     in the reference); the formulas in DESIGN.md §SDF are the spec.
+ */
+#ifndef RRTE_ORACLE_H
+#define RRTE_ORACLE_H
+
+#include "../include/rrte_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_hit {
+    float t;
+    float point[3];
+    float normal[3];
+    int32_t front_face;
+} oracle_hit;
+
+/* Render rows [row_begin, row_end) of the frame (whole image when both 0).
+ * out_rgba8 / out_f32 are full-frame W*H*4 buffers (either may be null).
+ * Returns 0 on success, nonzero on malformed input. */
+int rrte_oracle_render(const rrte_scene_ir* scene, const rrte_render_params* params,
+                       uint8_t* out_rgba8, float* out_f32, uint64_t* shadow_rays,
+                       int nthreads, uint32_t row_begin, uint32_t row_end);
+
+/* Known-answer-test hooks. */
+int rrte_oracle_intersect(const rrte_scene_ir* scene, uint32_t prim_index,
+                          const float origin[3], const float direction[3],
+                          float t_min, float t_max, oracle_hit* out);
+void rrte_oracle_generate_ray(const rrte_camera* cam, float u, float v,
+                              float origin_out[3], float dir_out[3]);
+void rrte_oracle_look_at(const float position[3], const float target[3],
+                         float quat_out[4]);
+float rrte_oracle_sdf_eval(const rrte_scene_ir* scene, uint32_t prim_index,
+                           const float p[3]);
+void rrte_oracle_mat4_srt(const float trs[10], float m_out[16]);
+void rrte_oracle_mat4_inverse(const float m[16], float inv_out[16]);
+float rrte_oracle_sinf(float x);
+float rrte_oracle_cosf(float x);
+float rrte_oracle_value_noise(float x, float y, float z, uint32_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

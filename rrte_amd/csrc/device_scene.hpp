@@ -1,0 +1,198 @@
+// device_scene.hpp — device-side scene records and f32 math for the gfx950
+// ray kernels.  Every arithmetic expression below keeps the operation order
+// of the reference (cited file:line, paths relative to Melthizar/RRTE) so the
+// kernel is bit-identical to the reference algorithm wherever the reference
+// is deterministic; the library is compiled with -ffp-contract=off and the
+// HIP default correctly-rounded f32 divide/sqrt.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rrte_hip.h"
+
+namespace rrte {
+
+// ------------------------------------------------------------------ records
+// Device copy of one SceneObject.  Read with wave-uniform indices, so the
+// compiler serves it from the scalar cache into SGPRs (s_load_dwordx*):
+// every lane of a wave tests the same object at the same time.
+struct alignas(16) DPrim {
+    uint32_t kind;
+    int32_t material;
+    uint32_t sdf_first;
+    uint32_t sdf_count;
+    uint32_t sdf_max_steps;
+    float sdf_step_scale;
+    float sdf_hit_eps;
+    uint32_t flags;          // bit0: transform is identity
+    float p[20];
+    float xf[12];            // Transform::to_matrix, columns x,y,z,w (xyz each)
+    float inv[12];           // Transform::inverse_matrix
+    float _pad[12];
+};
+static_assert(sizeof(DPrim) == 256, "DPrim layout");
+
+enum : uint32_t { DPRIM_IDENTITY_XF = 1u };
+
+struct alignas(16) DMaterial {
+    uint32_t kind;
+    float fuzz;
+    float ior;
+    float _pad0;
+    float albedo[4];
+};
+static_assert(sizeof(DMaterial) == 32, "DMaterial layout");
+
+struct alignas(16) DLight {
+    uint32_t kind;
+    float intensity, range, linear, quadratic, inner_angle, outer_angle, _pad0;
+    float position[4];
+    float direction[4];
+    float color[4];
+    float cI[4];             // color * intensity (light.rs:189), 4 channels
+};
+static_assert(sizeof(DLight) == 96, "DLight layout");
+
+// Per-launch constants, passed by value (kernel arguments land in SGPRs).
+struct KParams {
+    uint32_t width, height;
+    uint32_t spp, max_depth;
+    uint32_t jitter, seed, flags;
+    uint32_t num_prims, num_lights, num_materials;
+    // row mapping: local row r -> image row (band interleave for multi-GPU)
+    uint32_t rows;           // rows this launch renders
+    uint32_t band_rows;      // 0 = identity mapping
+    uint32_t nranks, rank;
+    float bg[4];
+    float t_min, bias, inv_gamma, inv_spp;
+    // camera
+    uint32_t projection;
+    float cam_pos[3];
+    float cam_rot[4];
+    float half_h, aspect;
+    float ortho_l, ortho_r, ortho_b, ortho_t;
+    float cam_xf[12];
+};
+
+// ---------------------------------------------------------------- f32 vec3
+struct f3 { float x, y, z; };
+
+__device__ __forceinline__ f3 V(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 vadd(f3 a, f3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 vsub(f3 a, f3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 vneg(f3 a) { return V(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ f3 vmuls(f3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 vdivs(f3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
+// glam Vec3::dot, left to right
+__device__ __forceinline__ float vdot(f3 a, f3 b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
+__device__ __forceinline__ float vlen2(f3 a) { return vdot(a, a); }
+__device__ __forceinline__ float vlen(f3 a) { return __builtin_sqrtf(vdot(a, a)); }
+// glam Vec3::normalize: self * (1 / length())
+__device__ __forceinline__ f3 vnorm(f3 a) { return vmuls(a, 1.0f / __builtin_sqrtf(vdot(a, a))); }
+__device__ __forceinline__ f3 vcross(f3 a, f3 b) {
+    return V(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+__device__ __forceinline__ f3 vld(const float* p) { return V(p[0], p[1], p[2]); }
+__device__ __forceinline__ float comp(f3 a, uint32_t i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+__device__ __forceinline__ f3 setcomp(f3 a, uint32_t i, float s) {
+    if (i == 0) a.x = s; else if (i == 1) a.y = s; else a.z = s;
+    return a;
+}
+__device__ __forceinline__ float mn(float a, float b) { return (b < a) ? b : a; }
+__device__ __forceinline__ float mx(float a, float b) { return (b > a) ? b : a; }
+__device__ __forceinline__ float clampf_(float x, float lo, float hi) { return mn(mx(x, lo), hi); }
+
+struct Ray { f3 o, d; };
+// Ray::new normalises (ray.rs:13-18); Ray::at (ray.rs:21-23)
+__device__ __forceinline__ Ray ray_new(f3 o, f3 d) { return Ray{o, vnorm(d)}; }
+__device__ __forceinline__ f3 ray_at(const Ray& r, float t) { return vadd(r.o, vmuls(r.d, t)); }
+
+struct Hit { float t; f3 p, n; bool front; };
+// HitInfo::new (ray.rs:45-56)
+__device__ __forceinline__ void hit_new(Hit& h, float t, f3 p, f3 outward, const Ray& r) {
+    h.t = t;
+    h.p = p;
+    h.front = vdot(r.d, outward) < 0.0f;
+    h.n = h.front ? outward : vneg(outward);
+}
+
+// Mat4 (3x4 affine part, columns x,y,z,w) transform_point3 / transform_vector3
+__device__ __forceinline__ f3 m_point(const float* m, f3 p) {
+    return V(((m[0] * p.x + m[3] * p.y) + m[6] * p.z) + m[9],
+             ((m[1] * p.x + m[4] * p.y) + m[7] * p.z) + m[10],
+             ((m[2] * p.x + m[5] * p.y) + m[8] * p.z) + m[11]);
+}
+__device__ __forceinline__ f3 m_vector(const float* m, f3 p) {
+    return V((m[0] * p.x + m[3] * p.y) + m[6] * p.z,
+             (m[1] * p.x + m[4] * p.y) + m[7] * p.z,
+             (m[2] * p.x + m[5] * p.y) + m[8] * p.z);
+}
+
+// Quat * Vec3 (glam mul_vec3a): v*(w*w - b.b) + b*((v.b)*2) + (b x v)*(w*2)
+__device__ __forceinline__ f3 quat_rotate(const float* q, f3 v) {
+    f3 b = V(q[0], q[1], q[2]);
+    float w = q[3];
+    float b2 = vdot(b, b);
+    float k0 = w * w - b2;
+    float k1 = vdot(v, b) * 2.0f;
+    float k2 = w * 2.0f;
+    f3 c = vcross(b, v);
+    return vadd(vadd(vmuls(v, k0), vmuls(b, k1)), vmuls(c, k2));
+}
+
+// ------------------------------------------------------ build-defined trig
+// Deterministic sin/cos shared bit-for-bit with the oracle.
+__device__ __forceinline__ void sincos_rrte(float x, float& so, float& co) {
+    float k = floorf(x * 0.636619772f + 0.5f);
+    float r = ((x - k * 1.5703125f) - k * 4.837512969970703125e-4f) - k * 7.549789948768648e-8f;
+    float r2 = r * r;
+    float s = r + (r * r2) * (-1.6666654611e-1f + r2 * (8.3321608736e-3f + r2 * -1.9515295891e-4f));
+    float c = (1.0f - 0.5f * r2) +
+              (r2 * r2) * (4.166664568298827e-2f + r2 * (-1.388731625493765e-3f + r2 * 2.443315711809948e-5f));
+    int q = ((int)k) & 3;
+    float s_ = s, c_ = c;
+    so = (q == 0) ? s_ : (q == 1) ? c_ : (q == 2) ? -s_ : -c_;
+    co = (q == 0) ? c_ : (q == 1) ? -s_ : (q == 2) ? -c_ : s_;
+}
+
+__device__ __forceinline__ float lattice(int32_t ix, int32_t iy, int32_t iz, uint32_t seed) {
+    uint32_t h = seed ^ ((uint32_t)ix * 0x8da6b343u) ^ ((uint32_t)iy * 0xd8163841u) ^ ((uint32_t)iz * 0xcb1ab31fu);
+    h = (h ^ (h >> 16)) * 0x7feb352du;
+    h = (h ^ (h >> 15)) * 0x846ca68bu;
+    h = h ^ (h >> 16);
+    return (float)(h >> 8) * 1.1920928955078125e-7f - 1.0f;
+}
+__device__ __forceinline__ float lerpf_(float a, float b, float t) { return a + (b - a) * t; }
+__device__ __forceinline__ float value_noise(float x, float y, float z, uint32_t seed) {
+    float fx0 = floorf(x), fy0 = floorf(y), fz0 = floorf(z);
+    int32_t ix = (int32_t)fx0, iy = (int32_t)fy0, iz = (int32_t)fz0;
+    float fx = x - fx0, fy = y - fy0, fz = z - fz0;
+    float ux = fx * fx * (3.0f - 2.0f * fx);
+    float uy = fy * fy * (3.0f - 2.0f * fy);
+    float uz = fz * fz * (3.0f - 2.0f * fz);
+    float c000 = lattice(ix, iy, iz, seed), c100 = lattice(ix + 1, iy, iz, seed);
+    float c010 = lattice(ix, iy + 1, iz, seed), c110 = lattice(ix + 1, iy + 1, iz, seed);
+    float c001 = lattice(ix, iy, iz + 1, seed), c101 = lattice(ix + 1, iy, iz + 1, seed);
+    float c011 = lattice(ix, iy + 1, iz + 1, seed), c111 = lattice(ix + 1, iy + 1, iz + 1, seed);
+    float x00 = lerpf_(c000, c100, ux), x10 = lerpf_(c010, c110, ux);
+    float x01 = lerpf_(c001, c101, ux), x11 = lerpf_(c011, c111, ux);
+    float y0 = lerpf_(x00, x10, uy), y1 = lerpf_(x01, x11, uy);
+    return lerpf_(y0, y1, uz);
+}
+
+// ---------------------------------------------------------------- RNG
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {
+    uint32_t s = v * 747796405u + 2891336453u;
+    uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
+    return (w >> 22u) ^ w;
+}
+__device__ __forceinline__ float rng_f32(uint32_t& st) {
+    st = st * 747796405u + 2891336453u;
+    uint32_t s = st;
+    uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
+    w = (w >> 22u) ^ w;
+    return (float)(w >> 8) * 5.9604644775390625e-8f;
+}
+
+}  // namespace rrte

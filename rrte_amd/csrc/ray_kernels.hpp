@@ -1,0 +1,819 @@
+// ray_kernels.hpp — the per-pixel ray->scene loop for gfx950 (CDNA4).
+//
+// One wave64 lane per pixel, one wave per 8x8 pixel tile (rays in a wave are
+// spatially coherent, so the wave-uniform object loop and the sphere-tracing
+// loop diverge little), 4 waves per 256-thread workgroup.  Scene records are
+// read with wave-uniform indices -> scalar loads into SGPRs; no MFMA (there is
+// no dense contraction on this path).  Operation order mirrors the reference
+// (file:line cited per function, paths relative to Melthizar/RRTE).
+#pragma once
+
+#include "device_scene.hpp"
+
+namespace rrte {
+
+constexpr float kInf = __builtin_huge_valf();
+
+struct SceneView {
+    const DPrim* __restrict__ prims;
+    const DMaterial* __restrict__ mats;
+    const DLight* __restrict__ lights;
+    const rrte_sdf_node* __restrict__ nodes;
+    uint32_t num_prims, num_lights, num_materials;
+};
+
+// ------------------------------------------------------------- SDF program
+__device__ __forceinline__ float len2f(float a, float b) { return __builtin_sqrtf(a * a + b * b); }
+__device__ __forceinline__ float len3f(float a, float b, float c) { return __builtin_sqrtf((a * a + b * b) + c * c); }
+
+__device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__ f, f3 p) {
+    f3 q = vsub(p, V(f[0], f[1], f[2]));
+    switch (op) {
+    case RRTE_SDF_SPHERE:
+        return len3f(q.x, q.y, q.z) - f[3];
+    case RRTE_SDF_BOX: {
+        float dx = fabsf(q.x) - f[4] * 0.5f, dy = fabsf(q.y) - f[5] * 0.5f, dz = fabsf(q.z) - f[6] * 0.5f;
+        float outside = len3f(mx(dx, 0.0f), mx(dy, 0.0f), mx(dz, 0.0f));
+        float inside = mn(mx(dx, mx(dy, dz)), 0.0f);
+        return outside + inside;
+    }
+    case RRTE_SDF_CYLINDER: {
+        float dx = len2f(q.x, q.z) - f[3], dy = fabsf(q.y) - f[4] * 0.5f;
+        return mn(mx(dx, dy), 0.0f) + len2f(mx(dx, 0.0f), mx(dy, 0.0f));
+    }
+    case RRTE_SDF_PRISM: {
+        float a = mx(fabsf(q.x) * 0.866025f + q.y * 0.5f, -q.y) - f[5] * 0.25f;
+        return mx(fabsf(q.z) - f[6] * 0.5f, a);
+    }
+    case RRTE_SDF_TORUS: {
+        float qx = len2f(q.x, q.z) - f[3];
+        return len2f(qx, q.y) - f[4];
+    }
+    case RRTE_SDF_TUBE: {
+        float rad = len2f(q.x, q.z);
+        float mid = (f[3] + f[4]) * 0.5f, half = (f[3] - f[4]) * 0.5f;
+        float dx = fabsf(rad - mid) - half, dy = fabsf(q.y) - f[5] * 0.5f;
+        return mn(mx(dx, dy), 0.0f) + len2f(mx(dx, 0.0f), mx(dy, 0.0f));
+    }
+    case RRTE_SDF_RING: {
+        float qx = len2f(q.x, q.y) - f[3];
+        return len2f(qx, q.z) - f[4];
+    }
+    case RRTE_SDF_CONE: {
+        float r1 = f[3], hh = f[4] * 0.5f;
+        float qx = len2f(q.x, q.z), qy = q.y;
+        float k2x = -r1, k2y = hh * 2.0f;
+        float cax = qx - mn(qx, (qy < 0.0f) ? r1 : 0.0f);
+        float cay = fabsf(qy) - hh;
+        float k1mqx = 0.0f - qx, k1mqy = hh - qy;
+        float tnum = k1mqx * k2x + k1mqy * k2y;
+        float tden = k2x * k2x + k2y * k2y;
+        float t = clampf_(tnum / tden, 0.0f, 1.0f);
+        float cbx = (qx - 0.0f) + k2x * t;
+        float cby = (qy - hh) + k2y * t;
+        float s = (cbx < 0.0f && cay < 0.0f) ? -1.0f : 1.0f;
+        float da = cax * cax + cay * cay, db = cbx * cbx + cby * cby;
+        return s * __builtin_sqrtf(mn(da, db));
+    }
+    case RRTE_SDF_CAPSULE: {
+        float hh = f[4] * 0.5f;
+        float y = q.y - clampf_(q.y, -hh, hh);
+        return len3f(q.x, y, q.z) - f[3];
+    }
+    case RRTE_SDF_ELLIPSOID: {
+        float rx = f[4], ry = f[5], rz = f[6];
+        float k0 = len3f(q.x / rx, q.y / ry, q.z / rz);
+        float k1 = len3f(q.x / (rx * rx), q.y / (ry * ry), q.z / (rz * rz));
+        if (!(k1 > 0.0f)) return -mn(rx, mn(ry, rz));
+        return k0 * (k0 - 1.0f) / k1;
+    }
+    default:
+        return kInf;
+    }
+}
+
+// smooth_min (README.md:485-488)
+__device__ __forceinline__ float smin(float a, float b, float k) {
+    float h = clampf_(0.5f + (0.5f * (b - a)) / k, 0.0f, 1.0f);
+    float om = 1.0f - h;
+    return (a * h + b * om) - (k * h) * om;
+}
+
+__device__ __forceinline__ f3 sdf_deform(uint32_t op, const uint32_t* __restrict__ iarg,
+                                         const float* __restrict__ f, f3 p) {
+    f3 c = V(f[0], f[1], f[2]);
+    f3 q = vsub(p, c);
+    switch (op) {
+    case RRTE_SDF_TWIST:
+    case RRTE_SDF_BEND: {
+        uint32_t ax = iarg[0];
+        uint32_t drive = (op == RRTE_SDF_TWIST) ? ax : iarg[1];
+        uint32_t u = (ax + 1) % 3, w = (ax + 2) % 3;
+        float s, co;
+        sincos_rrte(f[3] * comp(q, drive), s, co);
+        float qu = comp(q, u), qw = comp(q, w);
+        q = setcomp(q, u, co * qu - s * qw);
+        q = setcomp(q, w, s * qu + co * qw);
+        break;
+    }
+    case RRTE_SDF_TAPER: {
+        uint32_t ax = iarg[0];
+        uint32_t u = (ax + 1) % 3, w = (ax + 2) % 3;
+        float t = clampf_((comp(q, ax) + f[5] * 0.5f) / f[5], 0.0f, 1.0f);
+        float s = f[3] + (f[4] - f[3]) * t;
+        q = setcomp(q, u, comp(q, u) / s);
+        q = setcomp(q, w, comp(q, w) / s);
+        break;
+    }
+    case RRTE_SDF_NOISE: {
+        uint32_t oct = iarg[0], seed = iarg[1];
+        f3 x = vmuls(q, f[3]);
+        float acc[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            float amp = 1.0f, fr = 1.0f, sum = 0.0f;
+            for (uint32_t o = 0; o < oct; ++o) {
+                uint32_t sd = seed + (uint32_t)k * 0x9e3779b9u + o * 0x85ebca6bu;
+                sum = sum + amp * value_noise(x.x * fr, x.y * fr, x.z * fr, sd);
+                amp = amp * f[5];
+                fr = fr * 2.0f;
+            }
+            acc[k] = sum;
+        }
+        q = V(q.x + f[4] * acc[0], q.y + f[4] * acc[1], q.z + f[4] * acc[2]);
+        break;
+    }
+    case RRTE_SDF_WAVE: {
+        uint32_t ax = iarg[0], disp = iarg[1];
+        float s, co;
+        sincos_rrte(f[4] * comp(q, ax), s, co);
+        q = setcomp(q, disp, comp(q, disp) + f[3] * s);
+        break;
+    }
+    default:
+        break;
+    }
+    return vadd(q, c);
+}
+
+// Evaluate one SDFObject's postfix program at p.  The program counter, the
+// op and the stack pointers are wave-uniform (every lane runs the same
+// program), so the stacks are register arrays indexed by SGPR values.
+__device__ __forceinline__ float sdf_eval(const rrte_sdf_node* __restrict__ nodes, uint32_t count, f3 p) {
+    float vs[RRTE_SDF_MAX_STACK];
+    f3 ps[RRTE_SDF_MAX_POINT_STACK];
+    uint32_t sp = 0, pp = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        const rrte_sdf_node* __restrict__ n = &nodes[i];
+        uint32_t op = n->op;
+        if (op < 32) {
+            vs[sp] = sdf_leaf(op, n->f, p);
+            ++sp;
+        } else if (op < 64) {
+            float b = vs[sp - 1], a = vs[sp - 2], r;
+            float k = n->f[0];
+            switch (op) {
+            case RRTE_SDF_UNION: r = mn(a, b); break;
+            case RRTE_SDF_DIFFERENCE: r = mx(a, -b); break;
+            case RRTE_SDF_INTERSECTION: r = mx(a, b); break;
+            case RRTE_SDF_SMOOTH_UNION: r = smin(a, b, k); break;
+            case RRTE_SDF_SMOOTH_DIFFERENCE: r = -smin(-a, b, k); break;
+            default: r = -smin(-a, -b, k); break;
+            }
+            sp -= 2;
+            vs[sp] = r;
+            ++sp;
+        } else if (op < 96) {
+            ps[pp] = p;
+            ++pp;
+            p = sdf_deform(op, n->i, n->f, p);
+        } else {
+            --pp;
+            p = ps[pp];
+        }
+    }
+    return vs[0];
+}
+
+// SDFObject::intersect — sphere tracing inside the object's bounding sphere
+// (build-defined).  March steps and the four tetrahedral
+// normal samples share ONE evaluation site: a lane that has converged keeps
+// evaluating its normal samples while its neighbours are still marching, so
+// the wave never serialises a separate normal pass.  The per-lane trip count
+// diverges; the wave leaves the loop when its EXEC mask drains.
+// NEED_HIT = false (shadow rays) skips the normal samples entirely.
+template <bool NEED_HIT>
+__device__ __forceinline__ bool sdf_intersect(const SceneView& sc, const DPrim& pr, const Ray& r,
+                                              float t_min, float t_max, Hit& out) {
+    f3 bc = V(pr.p[0], pr.p[1], pr.p[2]);
+    float br = pr.p[3];
+    f3 oc = vsub(r.o, bc);
+    float b = vdot(oc, r.d);
+    float cc = vdot(oc, oc) - br * br;
+    float disc = b * b - cc;
+    if (disc < 0.0f) return false;
+    float sq = __builtin_sqrtf(disc);
+    float t = mx(t_min, -b - sq);
+    float tend = mn(t_max, -b + sq);
+    if (t > tend) return false;
+    const rrte_sdf_node* __restrict__ nodes = sc.nodes + pr.sdf_first;
+    const uint32_t count = pr.sdf_count;
+    const float eps = pr.sdf_hit_eps, scale = pr.sdf_step_scale;
+    const uint32_t steps = pr.sdf_max_steps;
+    if (steps == 0) return false;
+    const float h = 1e-3f;
+    f3 p = V(0.0f, 0.0f, 0.0f), n = V(0.0f, 0.0f, 0.0f);
+    uint32_t i = 0, phase = 0;  // phase 0: marching; 1..4: normal sample phase-1
+    bool result = false;
+    for (;;) {
+        f3 q;
+        if (phase == 0) {
+            q = ray_at(r, t);
+        } else {
+            // tetrahedron offsets k0=(+,-,-) k1=(-,-,+) k2=(-,+,-) k3=(+,+,+)
+            bool sx = (phase == 1) || (phase == 4);
+            bool sy = (phase >= 3);
+            bool sz = (phase == 2) || (phase == 4);
+            q = V(sx ? p.x + h : p.x - h, sy ? p.y + h : p.y - h, sz ? p.z + h : p.z - h);
+        }
+        float d = sdf_eval(nodes, count, q);
+        if (phase == 0) {
+            if (d < eps * t) {
+                if (!NEED_HIT) { result = true; break; }
+                p = q;
+                phase = 1;
+                continue;
+            }
+            t = t + d * scale;
+            ++i;
+            if (t > tend || i >= steps) break;
+        } else {
+            // n = k0 f0 + k1 f1 + k2 f2 + k3 f3, accumulated in the oracle's order
+            if (phase == 1) { n.x = d; n.y = -d; n.z = -d; }
+            else if (phase == 2) { n.x = n.x - d; n.y = n.y - d; n.z = n.z + d; }
+            else if (phase == 3) { n.x = n.x - d; n.y = n.y + d; n.z = n.z - d; }
+            else { n.x = n.x + d; n.y = n.y + d; n.z = n.z + d; }
+            ++phase;
+            if (phase == 5) { result = true; break; }
+        }
+    }
+    if (NEED_HIT && result) hit_new(out, t, p, vnorm(n), r);
+    return result;
+}
+
+// ----------------------------------------------------- analytic intersectors
+__device__ __forceinline__ void local_ray(const DPrim& pr, const Ray& r, Ray& lr) {
+    // inverse_matrix() applied to the ray, then Ray::new (primitives.rs:303-307)
+    lr = ray_new(m_point(pr.inv, r.o), vnorm(m_vector(pr.inv, r.d)));
+}
+
+// SceneObject::intersect (primitives.rs:57-725)
+template <bool NEED_HIT>
+__device__ __forceinline__ bool intersect(const SceneView& sc, const DPrim& pr, const Ray& r,
+                                          float t_min, float t_max, Hit& out) {
+    switch (pr.kind) {
+    case RRTE_PRIM_SPHERE: {  // primitives.rs:57-81
+        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+        float rad = pr.p[3];
+        f3 oc = vsub(r.o, ctr);
+        float a = vlen2(r.d);
+        float hb = vdot(oc, r.d);
+        float cc = vlen2(oc) - rad * rad;
+        float disc = hb * hb - a * cc;
+        if (disc < 0.0f) return false;
+        float sq = __builtin_sqrtf(disc);
+        float root = (-hb - sq) / a;
+        if (root < t_min || t_max < root) {
+            root = (-hb + sq) / a;
+            if (root < t_min || t_max < root) return false;
+        }
+        f3 p = ray_at(r, root);
+        hit_new(out, root, p, vdivs(vsub(p, ctr), rad), r);
+        return true;
+    }
+    case RRTE_PRIM_PLANE: {  // primitives.rs:133-149
+        f3 pt = V(pr.p[0], pr.p[1], pr.p[2]), n = V(pr.p[4], pr.p[5], pr.p[6]);
+        float denom = vdot(n, r.d);
+        if (fabsf(denom) < 1e-6f) return false;
+        float t = vdot(vsub(pt, r.o), n) / denom;
+        if (t < t_min || t > t_max) return false;
+        f3 p = ray_at(r, t);
+        hit_new(out, t, p, denom < 0.0f ? n : vneg(n), r);
+        return true;
+    }
+    case RRTE_PRIM_TRIANGLE: {  // primitives.rs:208-244
+        f3 v0 = V(pr.p[0], pr.p[1], pr.p[2]), v1 = V(pr.p[3], pr.p[4], pr.p[5]), v2 = V(pr.p[6], pr.p[7], pr.p[8]);
+        f3 e1 = vsub(v1, v0), e2 = vsub(v2, v0);
+        f3 h = vcross(r.d, e2);
+        float a = vdot(e1, h);
+        if (a > -1e-6f && a < 1e-6f) return false;
+        float f = 1.0f / a;
+        f3 s = vsub(r.o, v0);
+        float u = f * vdot(s, h);
+        if (u < 0.0f || u > 1.0f) return false;
+        f3 q = vcross(s, e1);
+        float v = f * vdot(r.d, q);
+        if (v < 0.0f || u + v > 1.0f) return false;
+        float t = f * vdot(e2, q);
+        if (t < t_min || t > t_max) return false;
+        f3 p = ray_at(r, t);
+        float w = 1.0f - u - v;
+        f3 n0 = V(pr.p[9], pr.p[10], pr.p[11]), n1 = V(pr.p[12], pr.p[13], pr.p[14]),
+           n2 = V(pr.p[15], pr.p[16], pr.p[17]);
+        f3 n = vnorm(vadd(vadd(vmuls(n0, w), vmuls(n1, u)), vmuls(n2, v)));
+        hit_new(out, t, p, n, r);
+        return true;
+    }
+    case RRTE_PRIM_CUBE: {  // primitives.rs:301-364
+        Ray lr;
+        local_ray(pr, r, lr);
+        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]), size = V(pr.p[4], pr.p[5], pr.p[6]);
+        f3 half = vmuls(size, 0.5f);
+        f3 mnb = vsub(ctr, half), mxb = vadd(ctr, half);
+        float t_near = t_min, t_far = t_max;
+        f3 normal = V(0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (uint32_t i = 0; i < 3; ++i) {
+            f3 axis = setcomp(V(0.0f, 0.0f, 0.0f), i, 1.0f);
+            float oc = vdot(lr.o, axis), dc = vdot(lr.d, axis);
+            float lo = vdot(mnb, axis), hi = vdot(mxb, axis);
+            if (fabsf(dc) < 1e-6f) {
+                if (oc < lo || oc > hi) return false;
+            } else {
+                float t1 = (lo - oc) / dc, t2 = (hi - oc) / dc;
+                float tsn = t1 < t2 ? t1 : t2, tsf = t1 < t2 ? t2 : t1;
+                if (tsn > t_near) {
+                    t_near = tsn;
+                    normal = t1 < t2 ? vneg(axis) : axis;
+                }
+                if (tsf < t_far) t_far = tsf;
+                if (t_near > t_far) return false;
+            }
+        }
+        float t = (t_near >= t_min) ? t_near : t_far;
+        if (t < t_min || t > t_max) return false;
+        f3 lp = ray_at(lr, t);
+        hit_new(out, t, m_point(pr.xf, lp), vnorm(m_vector(pr.xf, normal)), r);
+        return true;
+    }
+    case RRTE_PRIM_CYLINDER: {  // primitives.rs:419-465
+        Ray lr;
+        local_ray(pr, r, lr);
+        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+        float rad = pr.p[3], hh = pr.p[4] * 0.5f;
+        f3 oc = vsub(lr.o, ctr);
+        float a = lr.d.x * lr.d.x + lr.d.z * lr.d.z;
+        float b = 2.0f * (oc.x * lr.d.x + oc.z * lr.d.z);
+        float cc = oc.x * oc.x + oc.z * oc.z - rad * rad;
+        float disc = b * b - 4.0f * a * cc;
+        if (disc < 0.0f) return false;
+        float sq = __builtin_sqrtf(disc);
+        float ts0 = (-b - sq) / (2.0f * a), ts1 = (-b + sq) / (2.0f * a);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            float t = k == 0 ? ts0 : ts1;
+            if (t >= t_min && t <= t_max) {
+                f3 p = ray_at(lr, t);
+                if (fabsf(p.y - ctr.y) <= hh) {
+                    f3 ln = V((p.x - ctr.x) / rad, 0.0f, (p.z - ctr.z) / rad);
+                    hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
+                    return true;
+                }
+            }
+        }
+        return false;
+    }
+    case RRTE_PRIM_CONE: {  // primitives.rs:520-571
+        Ray lr;
+        local_ray(pr, r, lr);
+        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+        float rad = pr.p[3], ht = pr.p[4], hh = ht * 0.5f;
+        f3 oc = vsub(lr.o, ctr);
+        float k = rad / ht, k2 = k * k;
+        f3 d = lr.d;
+        float a = d.x * d.x + d.z * d.z - k2 * d.y * d.y;
+        float b = 2.0f * (oc.x * d.x + oc.z * d.z - k2 * (oc.y - hh) * d.y);
+        float cc = oc.x * oc.x + oc.z * oc.z - k2 * (oc.y - hh) * (oc.y - hh);
+        float disc = b * b - 4.0f * a * cc;
+        if (disc < 0.0f) return false;
+        float sq = __builtin_sqrtf(disc);
+        float ts0 = (-b - sq) / (2.0f * a), ts1 = (-b + sq) / (2.0f * a);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            float t = kk == 0 ? ts0 : ts1;
+            if (t >= t_min && t <= t_max) {
+                f3 p = ray_at(lr, t);
+                float yl = p.y - ctr.y;
+                if (yl >= -hh && yl <= hh) {
+                    float rr = __builtin_sqrtf(p.x * p.x + p.z * p.z);
+                    f3 ln = vnorm(V(p.x / rr, k, p.z / rr));
+                    hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
+                    return true;
+                }
+            }
+        }
+        return false;
+    }
+    case RRTE_PRIM_CAPSULE: {  // primitives.rs:626-725
+        Ray lr;
+        local_ray(pr, r, lr);
+        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+        float rad = pr.p[3], hh = pr.p[4] * 0.5f;
+        float closest = kInf;
+        bool found = false;
+        float a = vlen2(lr.d);
+#pragma unroll
+        for (int cap = 0; cap < 2; ++cap) {
+            f3 cc_ = cap == 0 ? vadd(ctr, V(0.0f, hh, 0.0f)) : vsub(ctr, V(0.0f, hh, 0.0f));
+            f3 oc = vsub(lr.o, cc_);
+            float hb = vdot(oc, lr.d);
+            float cc = vlen2(oc) - rad * rad;
+            float disc = hb * hb - a * cc;
+            if (disc >= 0.0f) {
+                float sq = __builtin_sqrtf(disc);
+                float ts0 = (-hb - sq) / a, ts1 = (-hb + sq) / a;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    float t = k == 0 ? ts0 : ts1;
+                    if (t >= t_min && t <= t_max && t < closest) {
+                        f3 p = ray_at(lr, t);
+                        bool ok = cap == 0 ? (p.y >= ctr.y) : (p.y <= ctr.y);
+                        if (ok) {
+                            f3 ln = vnorm(vsub(p, cc_));
+                            closest = t;
+                            hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
+                            found = true;
+                        }
+                    }
+                }
+            }
+        }
+        f3 oc = vsub(lr.o, ctr);
+        float ac = lr.d.x * lr.d.x + lr.d.z * lr.d.z;
+        float bc = 2.0f * (oc.x * lr.d.x + oc.z * lr.d.z);
+        float ccy = oc.x * oc.x + oc.z * oc.z - rad * rad;
+        float disc = bc * bc - 4.0f * ac * ccy;
+        if (disc >= 0.0f) {
+            float sq = __builtin_sqrtf(disc);
+            float ts0 = (-bc - sq) / (2.0f * ac), ts1 = (-bc + sq) / (2.0f * ac);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                float t = k == 0 ? ts0 : ts1;
+                if (t >= t_min && t <= t_max && t < closest) {
+                    f3 p = ray_at(lr, t);
+                    if (fabsf(p.y - ctr.y) <= hh) {
+                        f3 ln = V((p.x - ctr.x) / rad, 0.0f, (p.z - ctr.z) / rad);
+                        closest = t;
+                        hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
+                        found = true;
+                    }
+                }
+            }
+        }
+        return found;
+    }
+    case RRTE_PRIM_SDF:
+        return sdf_intersect<NEED_HIT>(sc, pr, r, t_min, t_max, out);
+    default:
+        return false;
+    }
+}
+
+// Closest hit over all objects (raytracer.rs:103-113): strict '<' keeps the
+// earlier object on ties; analytic objects get t_max = INFINITY as in the
+// reference, SDF objects march only up to the current closest hit.
+__device__ __forceinline__ int closest_hit(const SceneView& sc, const Ray& r, float t_min, Hit& best) {
+    int idx = -1;
+    for (uint32_t i = 0; i < sc.num_prims; ++i) {
+        const DPrim& pr = sc.prims[i];
+        Hit h;
+        float tmax = (pr.kind == RRTE_PRIM_SDF && idx >= 0) ? best.t : kInf;
+        if (intersect<true>(sc, pr, r, t_min, tmax, h)) {
+            if (idx < 0 || h.t < best.t) {
+                best = h;
+                idx = (int)i;
+            }
+        }
+    }
+    return idx;
+}
+
+// Any hit in [t_min, t_max] (LAMBERT_SHADOW shadow rays).
+__device__ __forceinline__ bool occluded(const SceneView& sc, const Ray& r, float t_min, float t_max) {
+    bool hit_any = false;
+    for (uint32_t i = 0; i < sc.num_prims; ++i) {
+        Hit h;
+        if (!hit_any && intersect<false>(sc, sc.prims[i], r, t_min, t_max, h)) hit_any = true;
+        if (__all(hit_any)) break;  // every active lane already occluded
+    }
+    return hit_any;
+}
+
+// --------------------------------------------------------------- lighting
+struct Contrib { float cr, cg, cb, ca; f3 dir; float dist, att; };
+
+// PointLight::calculate_attenuation (light.rs:170-178)
+__device__ __forceinline__ float point_att(const DLight& l, float d) {
+    if (d > l.range) return 0.0f;
+    float a = 1.0f / ((1.0f + l.linear * d) + (l.quadratic * d) * d);
+    return mx(a, 0.0f);
+}
+
+// Light::illuminate (light.rs:87-94, 182-194, 289-304, 365-372)
+__device__ __forceinline__ Contrib illuminate(const DLight& l, f3 p) {
+    Contrib k;
+    k.cr = l.cI[0]; k.cg = l.cI[1]; k.cb = l.cI[2]; k.ca = l.cI[3];
+    switch (l.kind) {
+    case RRTE_LIGHT_POINT: {
+        f3 lv = vsub(V(l.position[0], l.position[1], l.position[2]), p);
+        k.dist = vlen(lv);
+        k.dir = vnorm(lv);
+        k.att = point_att(l, k.dist);
+        break;
+    }
+    case RRTE_LIGHT_DIRECTIONAL:
+        k.dir = vneg(V(l.direction[0], l.direction[1], l.direction[2]));
+        k.dist = kInf;
+        k.att = 1.0f;
+        break;
+    case RRTE_LIGHT_SPOT: {
+        f3 lv = vsub(V(l.position[0], l.position[1], l.position[2]), p);
+        k.dist = vlen(lv);
+        k.dir = vnorm(lv);
+        float da = point_att(l, k.dist);
+        float ang = acosf(vdot(V(l.direction[0], l.direction[1], l.direction[2]), vneg(k.dir)));
+        float aa;
+        if (ang > l.outer_angle) aa = 0.0f;
+        else if (ang < l.inner_angle) aa = 1.0f;
+        else {
+            float fo = (l.outer_angle - ang) / (l.outer_angle - l.inner_angle);
+            aa = fo * fo;
+        }
+        k.att = da * aa;
+        break;
+    }
+    default:
+        k.dir = V(0.0f, 0.0f, 0.0f);
+        k.dist = 0.0f;
+        k.att = 1.0f;
+        break;
+    }
+    return k;
+}
+
+__device__ __forceinline__ f3 rand_in_unit_sphere(uint32_t& st) {  // vector.rs:35-46
+    for (;;) {
+        float x = rng_f32(st) * 2.0f - 1.0f;
+        float y = rng_f32(st) * 2.0f - 1.0f;
+        float z = rng_f32(st) * 2.0f - 1.0f;
+        f3 p = V(x, y, z);
+        if (vlen2(p) < 1.0f) return p;
+    }
+}
+__device__ __forceinline__ f3 reflect3(f3 v, f3 n) { return vsub(v, vmuls(n, 2.0f * vdot(v, n))); }
+
+// Material::scatter (material.rs:60-72, 99-110, 147-170, 200-202)
+__device__ __forceinline__ bool scatter(const DMaterial& m, const Ray& rin, const Hit& h, uint32_t& st, Ray& out) {
+    switch (m.kind) {
+    case RRTE_MAT_LAMBERTIAN: {
+        f3 sd = vadd(h.n, vnorm(rand_in_unit_sphere(st)));
+        f3 dir = vlen2(sd) < 1e-8f ? h.n : sd;
+        out = ray_new(h.p, dir);
+        return true;
+    }
+    case RRTE_MAT_METAL: {
+        f3 refl = reflect3(vnorm(rin.d), h.n);
+        f3 s = vadd(refl, vmuls(rand_in_unit_sphere(st), m.fuzz));
+        if (vdot(s, h.n) > 0.0f) { out = ray_new(h.p, s); return true; }
+        return false;
+    }
+    case RRTE_MAT_DIELECTRIC: {
+        float ratio = h.front ? 1.0f / m.ior : m.ior;
+        f3 ud = vnorm(rin.d);
+        float cos_t = mn(vdot(vneg(ud), h.n), 1.0f);
+        float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+        bool cannot = ratio * sin_t > 1.0f;
+        float r0 = (1.0f - ratio) / (1.0f + ratio);
+        r0 = r0 * r0;
+        float x = 1.0f - cos_t;
+        float x2 = x * x;
+        float refl = r0 + (1.0f - r0) * (x * (x2 * x2));
+        bool do_reflect = cannot;
+        if (!do_reflect) do_reflect = refl > rng_f32(st);
+        f3 dir;
+        if (do_reflect) {
+            dir = reflect3(ud, h.n);
+        } else {
+            float ct = mn(vdot(vneg(ud), h.n), 1.0f);
+            f3 perp = vmuls(vadd(ud, vmuls(h.n, ct)), ratio);
+            float l2 = vlen2(perp);
+            f3 par = vmuls(h.n, -__builtin_sqrtf(fabsf(1.0f - l2)));
+            dir = (l2 < 1.0f) ? vadd(perp, par) : reflect3(ud, h.n);
+        }
+        out = ray_new(h.p, dir);
+        return true;
+    }
+    default:
+        return false;
+    }
+}
+
+// ----------------------------------------------------------------- pixel
+struct Col { float r, g, b, a; };
+
+// Camera::generate_ray (camera.rs:98-133)
+__device__ __forceinline__ Ray generate_ray(const KParams& kp, float u, float v) {
+    float ndc_x = 2.0f * u - 1.0f;
+    float ndc_y = 1.0f - 2.0f * v;
+    if (kp.projection == RRTE_PERSPECTIVE) {
+        float half_w = kp.aspect * kp.half_h;
+        f3 cd = vnorm(V(ndc_x * half_w, ndc_y * kp.half_h, -1.0f));
+        f3 wd = quat_rotate(kp.cam_rot, cd);
+        return ray_new(V(kp.cam_pos[0], kp.cam_pos[1], kp.cam_pos[2]), wd);
+    }
+    float wx = kp.ortho_l + (kp.ortho_r - kp.ortho_l) * u;
+    float wy = kp.ortho_b + (kp.ortho_t - kp.ortho_b) * v;
+    f3 o = m_point(kp.cam_xf, V(wx, wy, 0.0f));
+    f3 wd = quat_rotate(kp.cam_rot, V(0.0f, 0.0f, -1.0f));
+    return ray_new(o, wd);
+}
+
+// Raytracer::ray_color (raytracer.rs:92-148) for one camera sample.
+// REFCOMPAT: ambient + sum(light.color*I*att) + albedo * ray_color(scatter).
+// The reference recursion color_d = local_d + albedo_d * color_{d+1} is
+// evaluated forward with a running albedo product; that is bit-identical to
+// the recursion for max_depth <= 2 (the parity configs use 1) and differs by
+// rounding only beyond.
+template <int MODE>
+__device__ __forceinline__ Col ray_color(const SceneView& sc, const KParams& kp, Ray r, uint32_t& st,
+                                         uint32_t& nshadow) {
+    Col out{0.0f, 0.0f, 0.0f, 1.0f};
+    if (kp.max_depth == 0) return out;
+    float tr = 1.0f, tg = 1.0f, tb = 1.0f;  // running albedo product
+    for (uint32_t depth = 0; depth < kp.max_depth; ++depth) {
+        Hit h;
+        int idx = closest_hit(sc, r, kp.t_min, h);
+        if (idx < 0) {
+            if (depth == 0) {
+                out = Col{kp.bg[0], kp.bg[1], kp.bg[2], kp.bg[3]};
+            } else {
+                out.r = out.r + tr * kp.bg[0];
+                out.g = out.g + tg * kp.bg[1];
+                out.b = out.b + tb * kp.bg[2];
+            }
+            break;
+        }
+        const DPrim& pr = sc.prims[idx];
+        int mi = pr.material;
+        if (mi < 0 || (uint32_t)mi >= sc.num_materials) break;  // BLACK
+        const DMaterial& m = sc.mats[mi];
+        float ar = m.albedo[0], ag = m.albedo[1], ab = m.albedo[2], aa = m.albedo[3];
+        // BLACK + ambient_color()*0.1 (raytracer.rs:124, material.rs:10-12)
+        float cr = 0.0f + (ar * 0.1f) * 0.1f;
+        float cg = 0.0f + (ag * 0.1f) * 0.1f;
+        float cb = 0.0f + (ab * 0.1f) * 0.1f;
+        float ca = 1.0f + (aa * 0.1f) * 0.1f;
+        if (MODE == RRTE_MODE_REFCOMPAT) {
+            for (uint32_t li = 0; li < sc.num_lights; ++li) {
+                Contrib k = illuminate(sc.lights[li], h.p);
+                cr = cr + k.cr * k.att;
+                cg = cg + k.cg * k.att;
+                cb = cb + k.cb * k.att;
+                ca = ca + k.ca * k.att;
+            }
+        } else {
+            const float bias = kp.bias;
+            for (uint32_t li = 0; li < sc.num_lights; ++li) {
+                const DLight& l = sc.lights[li];
+                Contrib k = illuminate(l, h.p);
+                if (l.kind == RRTE_LIGHT_AMBIENT) {
+                    cr = cr + ar * k.cr;
+                    cg = cg + ag * k.cg;
+                    cb = cb + ab * k.cb;
+                    continue;
+                }
+                float ndl = vdot(h.n, k.dir);
+                if (ndl > 0.0f && k.att > 0.0f) {
+                    ++nshadow;
+                    Ray sr = ray_new(vadd(h.p, vmuls(h.n, bias)), k.dir);
+                    if (!occluded(sc, sr, bias, k.dist)) {
+                        float f = k.att * ndl;
+                        cr = cr + ar * (k.cr * f);
+                        cg = cg + ag * (k.cg * f);
+                        cb = cb + ab * (k.cb * f);
+                    }
+                }
+            }
+        }
+        if (depth == 0) {
+            out = Col{cr, cg, cb, ca};
+        } else {
+            out.r = out.r + tr * cr;
+            out.g = out.g + tg * cg;
+            out.b = out.b + tb * cb;
+        }
+        if (MODE != RRTE_MODE_REFCOMPAT) break;  // direct lighting only
+        Ray sc_ray;
+        if (!scatter(m, r, h, st, sc_ray)) break;
+        if (depth == 0) out.a = out.a + 1.0f;  // Color::from(Vec3) has alpha 1 (color.rs:78-82)
+        if (depth + 1 >= kp.max_depth) break;   // ray_color(depth 0) == BLACK: adds 0
+        tr = tr * ar;
+        tg = tg * ag;
+        tb = tb * ab;
+        r = sc_ray;
+    }
+    return out;
+}
+
+// Rust `(x * 255.0) as u8` (raytracer.rs:82-85) and f32::clamp (color.rs:48-55)
+__device__ __forceinline__ uint32_t to_u8(float c) {
+    float v = c * 255.0f;
+    if (!(v > 0.0f)) return 0u;
+    if (v >= 255.0f) return 255u;
+    return (uint32_t)v;
+}
+__device__ __forceinline__ float rclamp(float x) {
+    if (x < 0.0f) return 0.0f;
+    if (x > 1.0f) return 1.0f;
+    return x;
+}
+
+// Map this launch's local row to the image row (band interleave, §8e).
+__device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
+    if (kp.band_rows == 0) return r;
+    uint32_t b = r / kp.band_rows, w = r - b * kp.band_rows;
+    return (b * kp.nranks + kp.rank) * kp.band_rows + w;
+}
+
+// One lane per pixel; wave = 8x8 tile, workgroup = 16x16 pixels.
+template <int MODE>
+__global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, uint32_t* __restrict__ out_rgba8,
+                                                  float4* __restrict__ out_f32,
+                                                  unsigned long long* __restrict__ counters) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t lr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    uint32_t nshadow = 0;
+    if (x < kp.width && lr < kp.rows) {
+        const uint32_t y = image_row(kp, lr);
+        const uint32_t pix = y * kp.width + x;
+        Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
+        for (uint32_t s = 0; s < kp.spp; ++s) {
+            uint32_t st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
+            float jx = 0.5f, jy = 0.5f;
+            if (kp.jitter == RRTE_JITTER_RANDOM) {
+                jx = rng_f32(st);
+                jy = rng_f32(st);
+            }
+            float u = ((float)x + jx) / (float)kp.width;
+            float v = ((float)y + jy) / (float)kp.height;
+            Ray r = generate_ray(kp, u, v);
+            Col c = ray_color<MODE>(sc, kp, r, st, nshadow);
+            acc.r = acc.r + c.r;
+            acc.g = acc.g + c.g;
+            acc.b = acc.b + c.b;
+            acc.a = acc.a + c.a;
+        }
+        acc.r = acc.r * kp.inv_spp;
+        acc.g = acc.g * kp.inv_spp;
+        acc.b = acc.b * kp.inv_spp;
+        acc.a = acc.a * kp.inv_spp;
+        const float ig = kp.inv_gamma;
+        float gr = rclamp(powf(acc.r, ig)), gg = rclamp(powf(acc.g, ig)), gb = rclamp(powf(acc.b, ig));
+        float ga = rclamp(acc.a);
+        const size_t o = (size_t)lr * kp.width + x;  // packed local rows
+        if (out_rgba8)
+            out_rgba8[o] = to_u8(gr) | (to_u8(gg) << 8) | (to_u8(gb) << 16) | (to_u8(ga) << 24);
+        if (out_f32) {
+            if (kp.flags & RRTE_FLAG_F32_LINEAR)
+                out_f32[o] = make_float4(acc.r, acc.g, acc.b, acc.a);
+            else
+                out_f32[o] = make_float4(gr, gg, gb, ga);
+        }
+    }
+    if (MODE != RRTE_MODE_REFCOMPAT) {
+        // wave-reduce the shadow-ray count, one atomic per wave
+        uint32_t v = nshadow;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0 && v) atomicAdd(counters, (unsigned long long)v);
+    }
+}
+
+// Root-side de-interleave after the RCCL gather: the gathered buffer holds
+// each rank's packed rows (rank-major, `rows_cap` rows per rank).
+__global__ __launch_bounds__(256) void deinterleave_kernel(const uint32_t* __restrict__ gathered,
+                                                           uint32_t* __restrict__ full, uint32_t width,
+                                                           uint32_t height, uint32_t band_rows,
+                                                           uint32_t nranks, uint32_t rows_cap) {
+    const uint32_t y = blockIdx.y;
+    const uint32_t band = y / band_rows, w = y - band * band_rows;
+    const uint32_t rank = band % nranks, local_band = band / nranks;
+    const uint32_t lr = local_band * band_rows + w;
+    const uint32_t* src = gathered + ((size_t)rank * rows_cap + lr) * width;
+    uint32_t* dst = full + (size_t)y * width;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < width; x += gridDim.x * blockDim.x) dst[x] = src[x];
+    (void)height;
+}
+
+}  // namespace rrte

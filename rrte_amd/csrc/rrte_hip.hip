@@ -1,0 +1,594 @@
+// rrte_hip.hip — C-ABI implementation (include/rrte_hip.h) of the MI355X-native
+// replacement for rrte-renderer's Raytracer::render
+// (Melthizar/RRTE crates/rrte-renderer/src/raytracer.rs:45-148).
+//
+// Host side: validate + lower rrte_scene_ir to device records (precomputing the
+// per-object Transform matrices the reference rebuilds per ray,
+// primitives.rs:303,421,522,628), cache them in HBM until the scene changes,
+// launch the ray kernel, and (multi-GPU) gather interleaved row bands to the
+// root over RCCL/xGMI.  No exception crosses the ABI.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ray_kernels.hpp"
+
+using namespace rrte;
+
+struct rrte_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    std::string err;
+    // scene cache (device copy + the host bytes it was made from)
+    std::vector<unsigned char> scene_key;
+    DPrim* d_prims = nullptr; size_t cap_prims = 0;
+    DMaterial* d_mats = nullptr; size_t cap_mats = 0;
+    DLight* d_lights = nullptr; size_t cap_lights = 0;
+    rrte_sdf_node* d_nodes = nullptr; size_t cap_nodes = 0;
+    uint32_t n_prims = 0, n_mats = 0, n_lights = 0, n_nodes = 0;
+    // frame buffers for the blocking entry points
+    uint32_t* d_rgba = nullptr; size_t cap_rgba = 0;
+    float4* d_f32 = nullptr; size_t cap_f32 = 0;
+    unsigned long long* d_counters = nullptr;   // [0] shadow rays (accumulating)
+    unsigned long long* h_counters = nullptr;   // pinned
+    unsigned long long shadow_base = 0;         // value at the start of the last frame
+    // multi-GPU
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    uint32_t* d_gather = nullptr; size_t cap_gather = 0;
+    uint32_t* d_full = nullptr; size_t cap_full = 0;
+    bool gather_timed = false;
+    rrte_stats stats{};
+    bool pending_kernel_timing = false;
+    uint64_t pending_primary = 0;
+};
+
+namespace {
+
+rrte_status fail(rrte_ctx* c, rrte_status st, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return st;
+}
+
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail((ctx), RRTE_HIP_ERROR, "%s failed: %s", #expr, hipGetErrorString(e_));     \
+    } while (0)
+
+#define NCCLCHK(ctx, expr)                                                                         \
+    do {                                                                                           \
+        ncclResult_t r_ = (expr);                                                                  \
+        if (r_ != ncclSuccess)                                                                     \
+            return fail((ctx), RRTE_RCCL_ERROR, "%s failed: %s", #expr, ncclGetErrorString(r_));   \
+    } while (0)
+
+template <typename T>
+rrte_status ensure(rrte_ctx* c, T*& ptr, size_t& cap, size_t n) {
+    if (n <= cap && ptr) return RRTE_OK;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    size_t want = n < 1 ? 1 : n;
+    HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&ptr), want * sizeof(T)));
+    cap = want;
+    return RRTE_OK;
+}
+
+// ---- glam restatement on the host (same algorithms as oracle/, see there) ----
+void mat4_srt(const float trs[10], float m[16]) {
+    float x = trs[3], y = trs[4], z = trs[5], w = trs[6];
+    float x2 = x + x, y2 = y + y, z2 = z + z;
+    float xx = x * x2, xy = x * y2, xz = x * z2;
+    float yy = y * y2, yz = y * z2, zz = z * z2;
+    float wx = w * x2, wy = w * y2, wz = w * z2;
+    float sx = trs[7], sy = trs[8], sz = trs[9];
+    const float cols[3][3] = {{1.0f - (yy + zz), xy + wz, xz - wy},
+                              {xy - wz, 1.0f - (xx + zz), yz + wx},
+                              {xz + wy, yz - wx, 1.0f - (xx + yy)}};
+    const float sc[3] = {sx, sy, sz};
+    for (int c = 0; c < 3; ++c) {
+        for (int r = 0; r < 3; ++r) m[c * 4 + r] = cols[c][r] * sc[c];
+        m[c * 4 + 3] = 0.0f * sc[c];
+    }
+    m[12] = trs[0]; m[13] = trs[1]; m[14] = trs[2]; m[15] = 1.0f;
+}
+
+// glam Mat4::inverse (glm cofactor form), transform.rs:55-57
+void mat4_inverse(const float* a, float* out) {
+    auto M = [a](int c, int r) { return a[c * 4 + r]; };
+    const float coef[18] = {
+        M(2, 2) * M(3, 3) - M(3, 2) * M(2, 3), M(1, 2) * M(3, 3) - M(3, 2) * M(1, 3),
+        M(1, 2) * M(2, 3) - M(2, 2) * M(1, 3), M(2, 1) * M(3, 3) - M(3, 1) * M(2, 3),
+        M(1, 1) * M(3, 3) - M(3, 1) * M(1, 3), M(1, 1) * M(2, 3) - M(2, 1) * M(1, 3),
+        M(2, 1) * M(3, 2) - M(3, 1) * M(2, 2), M(1, 1) * M(3, 2) - M(3, 1) * M(1, 2),
+        M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2), M(2, 0) * M(3, 3) - M(3, 0) * M(2, 3),
+        M(1, 0) * M(3, 3) - M(3, 0) * M(1, 3), M(1, 0) * M(2, 3) - M(2, 0) * M(1, 3),
+        M(2, 0) * M(3, 2) - M(3, 0) * M(2, 2), M(1, 0) * M(3, 2) - M(3, 0) * M(1, 2),
+        M(1, 0) * M(2, 2) - M(2, 0) * M(1, 2), M(2, 0) * M(3, 1) - M(3, 0) * M(2, 1),
+        M(1, 0) * M(3, 1) - M(3, 0) * M(1, 1), M(1, 0) * M(2, 1) - M(2, 0) * M(1, 1)};
+    // Fac_k = (c_a, c_a, c_b, c_c) in glm's numbering
+    const float fac[6][4] = {{coef[0], coef[0], coef[1], coef[2]},     {coef[3], coef[3], coef[4], coef[5]},
+                             {coef[6], coef[6], coef[7], coef[8]},     {coef[9], coef[9], coef[10], coef[11]},
+                             {coef[12], coef[12], coef[13], coef[14]}, {coef[15], coef[15], coef[16], coef[17]}};
+    const float vec[4][4] = {{M(1, 0), M(0, 0), M(0, 0), M(0, 0)},
+                             {M(1, 1), M(0, 1), M(0, 1), M(0, 1)},
+                             {M(1, 2), M(0, 2), M(0, 2), M(0, 2)},
+                             {M(1, 3), M(0, 3), M(0, 3), M(0, 3)}};
+    float inv[16];
+    for (int i = 0; i < 4; ++i) {
+        float sa = (i & 1) ? -1.0f : 1.0f, sb = -sa;
+        inv[0 * 4 + i] = ((vec[1][i] * fac[0][i] - vec[2][i] * fac[1][i]) + vec[3][i] * fac[2][i]) * sa;
+        inv[1 * 4 + i] = ((vec[0][i] * fac[0][i] - vec[2][i] * fac[3][i]) + vec[3][i] * fac[4][i]) * sb;
+        inv[2 * 4 + i] = ((vec[0][i] * fac[1][i] - vec[1][i] * fac[3][i]) + vec[3][i] * fac[5][i]) * sa;
+        inv[3 * 4 + i] = ((vec[0][i] * fac[2][i] - vec[1][i] * fac[4][i]) + vec[2][i] * fac[5][i]) * sb;
+    }
+    float d0 = M(0, 0) * inv[0], d1 = M(0, 1) * inv[4], d2 = M(0, 2) * inv[8], d3 = M(0, 3) * inv[12];
+    float det = (d0 + d1) + (d2 + d3);
+    float rdet = 1.0f / det;
+    for (int i = 0; i < 16; ++i) out[i] = inv[i] * rdet;
+}
+
+void to_affine12(const float* m16, float* m12) {
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 3; ++r) m12[c * 3 + r] = m16[c * 4 + r];
+}
+
+bool sdf_program_ok(const rrte_sdf_node* nodes, uint32_t count) {
+    int sp = 0, pp = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        uint32_t op = nodes[i].op;
+        if (op >= RRTE_SDF_SPHERE && op <= RRTE_SDF_ELLIPSOID) {
+            if (++sp > RRTE_SDF_MAX_STACK) return false;
+        } else if (op >= RRTE_SDF_UNION && op <= RRTE_SDF_SMOOTH_INTERSECTION) {
+            if (sp < 2) return false;
+            --sp;
+        } else if (op >= RRTE_SDF_BEND && op <= RRTE_SDF_WAVE) {
+            if (++pp > RRTE_SDF_MAX_POINT_STACK) return false;
+            if ((op == RRTE_SDF_BEND || op == RRTE_SDF_TWIST || op == RRTE_SDF_TAPER || op == RRTE_SDF_WAVE) &&
+                (nodes[i].i[0] > 2 || nodes[i].i[1] > 2))
+                return false;
+            if (op == RRTE_SDF_NOISE && nodes[i].i[0] > RRTE_SDF_MAX_OCTAVES) return false;
+        } else if (op == RRTE_SDF_POP_POINT) {
+            if (pp < 1) return false;
+            --pp;
+        } else {
+            return false;
+        }
+    }
+    return sp == 1 && pp == 0;
+}
+
+rrte_status validate(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p) {
+    if (!s || !p) return fail(c, RRTE_INVALID_ARG, "null scene or params");
+    if (p->width == 0 || p->height == 0) return fail(c, RRTE_INVALID_ARG, "zero-sized frame %ux%u", p->width, p->height);
+    if ((uint64_t)p->width * p->height > (1ull << 30)) return fail(c, RRTE_INVALID_ARG, "frame too large");
+    if (p->samples_per_pixel == 0) return fail(c, RRTE_INVALID_ARG, "samples_per_pixel must be >= 1");
+    if (p->mode > RRTE_MODE_LAMBERT_SHADOW) return fail(c, RRTE_INVALID_ARG, "unknown mode %u", p->mode);
+    if (p->jitter > RRTE_JITTER_RANDOM) return fail(c, RRTE_INVALID_ARG, "unknown jitter %u", p->jitter);
+    if ((s->num_prims && !s->prims) || (s->num_lights && !s->lights) || (s->num_materials && !s->materials) ||
+        (s->num_sdf_nodes && !s->sdf_nodes))
+        return fail(c, RRTE_INVALID_ARG, "null array with nonzero count");
+    if (s->camera.projection > RRTE_ORTHOGRAPHIC) return fail(c, RRTE_INVALID_ARG, "unknown projection");
+    for (uint32_t i = 0; i < s->num_prims; ++i) {
+        const rrte_prim& pr = s->prims[i];
+        if (pr.kind > RRTE_PRIM_SDF) return fail(c, RRTE_UNSUPPORTED_PRIM, "prim %u: unknown kind %u", i, pr.kind);
+        if (pr.kind == RRTE_PRIM_SDF) {
+            if ((uint64_t)pr.sdf_first + pr.sdf_count > s->num_sdf_nodes)
+                return fail(c, RRTE_INVALID_ARG, "prim %u: SDF node range out of bounds", i);
+            if (!sdf_program_ok(s->sdf_nodes + pr.sdf_first, pr.sdf_count))
+                return fail(c, RRTE_INVALID_ARG, "prim %u: malformed SDF program", i);
+        }
+    }
+    for (uint32_t i = 0; i < s->num_lights; ++i)
+        if (s->lights[i].kind > RRTE_LIGHT_AMBIENT)
+            return fail(c, RRTE_UNSUPPORTED_PRIM, "light %u: unknown kind %u", i, s->lights[i].kind);
+    for (uint32_t i = 0; i < s->num_materials; ++i)
+        if (s->materials[i].kind > RRTE_MAT_EMISSIVE)
+            return fail(c, RRTE_UNSUPPORTED_PRIM, "material %u: unknown kind %u", i, s->materials[i].kind);
+    return RRTE_OK;
+}
+
+// Upload the scene if it differs from the cached copy (the analogue of
+// caching on Scene::is_dirty, crates/rrte-scene/src/lib.rs:310-312).
+rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
+    const size_t bp = sizeof(rrte_prim) * s->num_prims, bm = sizeof(rrte_material) * s->num_materials,
+                 bl = sizeof(rrte_light) * s->num_lights, bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
+    const size_t key_len = bp + bm + bl + bn + 4 * sizeof(uint32_t);
+    bool same = c->scene_key.size() == key_len;
+    if (same) {
+        const unsigned char* k = c->scene_key.data();
+        same = (bp == 0 || !memcmp(k, s->prims, bp)) && (bm == 0 || !memcmp(k + bp, s->materials, bm)) &&
+               (bl == 0 || !memcmp(k + bp + bm, s->lights, bl)) &&
+               (bn == 0 || !memcmp(k + bp + bm + bl, s->sdf_nodes, bn));
+    }
+    *upload_ms = 0.0;
+    if (same) return RRTE_OK;
+
+    std::vector<DPrim> prims(s->num_prims);
+    for (uint32_t i = 0; i < s->num_prims; ++i) {
+        const rrte_prim& in = s->prims[i];
+        DPrim& o = prims[i];
+        memset(&o, 0, sizeof o);
+        o.kind = in.kind;
+        o.material = in.material;
+        o.sdf_first = in.sdf_first;
+        o.sdf_count = in.sdf_count;
+        o.sdf_max_steps = in.sdf_max_steps;
+        o.sdf_step_scale = in.sdf_step_scale;
+        o.sdf_hit_eps = in.sdf_hit_eps;
+        memcpy(o.p, in.p, sizeof o.p);
+        float m[16], inv[16];
+        mat4_srt(in.trs, m);
+        mat4_inverse(m, inv);
+        to_affine12(m, o.xf);
+        to_affine12(inv, o.inv);
+    }
+    std::vector<DMaterial> mats(s->num_materials);
+    for (uint32_t i = 0; i < s->num_materials; ++i) {
+        static_assert(sizeof(rrte_material) == sizeof(DMaterial), "material layout");
+        memcpy(&mats[i], &s->materials[i], sizeof(DMaterial));
+    }
+    std::vector<DLight> lights(s->num_lights);
+    for (uint32_t i = 0; i < s->num_lights; ++i) {
+        const rrte_light& in = s->lights[i];
+        DLight& o = lights[i];
+        memset(&o, 0, sizeof o);
+        o.kind = in.kind;
+        o.intensity = in.intensity;
+        o.range = in.range;
+        o.linear = in.linear;
+        o.quadratic = in.quadratic;
+        o.inner_angle = in.inner_angle;
+        o.outer_angle = in.outer_angle;
+        memcpy(o.position, in.position, sizeof o.position);
+        memcpy(o.direction, in.direction, sizeof o.direction);
+        memcpy(o.color, in.color, sizeof o.color);
+        for (int k = 0; k < 4; ++k) o.cI[k] = in.color[k] * in.intensity;  // Color * f32 (light.rs:189)
+    }
+    rrte_status r;
+    if ((r = ensure(c, c->d_prims, c->cap_prims, prims.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, c->d_mats, c->cap_mats, mats.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, c->d_lights, c->cap_lights, lights.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, c->d_nodes, c->cap_nodes, (size_t)s->num_sdf_nodes)) != RRTE_OK) return r;
+    HIPCHK(c, hipEventRecord(c->ev2, st));
+    if (!prims.empty()) HIPCHK(c, hipMemcpyAsync(c->d_prims, prims.data(), prims.size() * sizeof(DPrim), hipMemcpyHostToDevice, st));
+    if (!mats.empty()) HIPCHK(c, hipMemcpyAsync(c->d_mats, mats.data(), mats.size() * sizeof(DMaterial), hipMemcpyHostToDevice, st));
+    if (!lights.empty()) HIPCHK(c, hipMemcpyAsync(c->d_lights, lights.data(), lights.size() * sizeof(DLight), hipMemcpyHostToDevice, st));
+    if (bn) HIPCHK(c, hipMemcpyAsync(c->d_nodes, s->sdf_nodes, bn, hipMemcpyHostToDevice, st));
+    // the staging vectors die at return: make the copies complete first
+    HIPCHK(c, hipStreamSynchronize(st));
+    HIPCHK(c, hipEventRecord(c->ev0, st));
+    HIPCHK(c, hipEventSynchronize(c->ev0));
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, c->ev2, c->ev0);
+    *upload_ms = ms;
+    c->n_prims = s->num_prims;
+    c->n_mats = s->num_materials;
+    c->n_lights = s->num_lights;
+    c->n_nodes = s->num_sdf_nodes;
+    c->scene_key.resize(key_len);
+    unsigned char* k = c->scene_key.data();
+    if (bp) memcpy(k, s->prims, bp);
+    if (bm) memcpy(k + bp, s->materials, bm);
+    if (bl) memcpy(k + bp + bm, s->lights, bl);
+    if (bn) memcpy(k + bp + bm + bl, s->sdf_nodes, bn);
+    return RRTE_OK;
+}
+
+KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows) {
+    KParams k;
+    memset(&k, 0, sizeof k);
+    k.width = p->width;
+    k.height = p->height;
+    k.spp = p->samples_per_pixel;
+    k.max_depth = p->max_depth;
+    k.jitter = p->jitter;
+    k.seed = p->seed;
+    k.flags = p->flags;
+    k.num_prims = s->num_prims;
+    k.num_lights = s->num_lights;
+    k.num_materials = s->num_materials;
+    k.rows = rows;
+    k.band_rows = c->nranks > 1 ? p->band_rows : 0;
+    k.nranks = (uint32_t)c->nranks;
+    k.rank = (uint32_t)c->rank;
+    memcpy(k.bg, p->background, sizeof k.bg);
+    k.t_min = p->t_min;
+    k.bias = p->shadow_bias;
+    k.inv_gamma = 1.0f / p->gamma;                        // raytracer.rs:79 -> color.rs:60
+    k.inv_spp = 1.0f / (float)p->samples_per_pixel;       // raytracer.rs:76
+    const rrte_camera& cam = s->camera;
+    k.projection = cam.projection;
+    memcpy(k.cam_pos, cam.position, sizeof k.cam_pos);
+    memcpy(k.cam_rot, cam.rotation, sizeof k.cam_rot);
+    k.half_h = tanf(cam.fov * 0.5f);                      // camera.rs:104
+    k.aspect = cam.aspect_ratio;
+    k.ortho_l = cam.left; k.ortho_r = cam.right; k.ortho_b = cam.bottom; k.ortho_t = cam.top;
+    float trs[10] = {cam.position[0], cam.position[1], cam.position[2], cam.rotation[0], cam.rotation[1],
+                     cam.rotation[2], cam.rotation[3], cam.scale[0], cam.scale[1], cam.scale[2]};
+    float m[16];
+    mat4_srt(trs, m);
+    to_affine12(m, k.cam_xf);
+    return k;
+}
+
+uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank) {
+    if (nranks <= 1 || band_rows == 0) return height;
+    uint32_t nb = (height + band_rows - 1) / band_rows, rows = 0;
+    for (uint32_t b = (uint32_t)rank; b < nb; b += (uint32_t)nranks) {
+        uint32_t r0 = b * band_rows, r1 = r0 + band_rows < height ? r0 + band_rows : height;
+        rows += r1 - r0;
+    }
+    return rows;
+}
+
+rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
+                   uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
+    KParams k = make_params(c, s, p, rows);
+    SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, s->num_prims, s->num_lights, s->num_materials};
+    dim3 grid((p->width + 15) / 16, (rows + 15) / 16), block(256);
+    if (rows == 0) return RRTE_OK;
+    if (p->mode == RRTE_MODE_REFCOMPAT)
+        hipLaunchKernelGGL(ray_kernel<RRTE_MODE_REFCOMPAT>, grid, block, 0, st, k, sv, d_rgba, d_f32, c->d_counters);
+    else
+        hipLaunchKernelGGL(ray_kernel<RRTE_MODE_LAMBERT_SHADOW>, grid, block, 0, st, k, sv, d_rgba, d_f32, c->d_counters);
+    HIPCHK(c, hipGetLastError());
+    return RRTE_OK;
+}
+
+// Read back the device counters and close the frame's statistics.
+rrte_status finish_frame(rrte_ctx* c) {
+    HIPCHK(c, hipMemcpyAsync(c->h_counters, c->d_counters, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->stats.shadow_rays = c->h_counters[0] - c->shadow_base;
+    c->shadow_base = c->h_counters[0];
+    if (c->pending_kernel_timing) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->stats.kernel_ms = ms;
+        c->pending_kernel_timing = false;
+    }
+    c->stats.primary_rays = c->pending_primary;
+    return RRTE_OK;
+}
+
+rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out8,
+                          float* outf) {
+    rrte_status r = validate(c, s, p);
+    if (r != RRTE_OK) return r;
+    HIPCHK(c, hipSetDevice(c->device));
+    double up = 0.0;
+    if ((r = upload_scene(c, s, c->stream, &up)) != RRTE_OK) return r;
+    const size_t npix = (size_t)p->width * p->height;
+    if ((r = ensure(c, c->d_rgba, c->cap_rgba, npix)) != RRTE_OK) return r;
+    if (outf && (r = ensure(c, c->d_f32, c->cap_f32, npix)) != RRTE_OK) return r;
+    // single-context render: all rows, no band mapping
+    const int nr = c->nranks, rk = c->rank;
+    c->nranks = 1;
+    c->rank = 0;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    r = launch(c, s, p, p->height, c->d_rgba, outf ? c->d_f32 : nullptr, c->stream);
+    c->nranks = nr;
+    c->rank = rk;
+    if (r != RRTE_OK) return r;
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->pending_kernel_timing = true;
+    c->pending_primary = (uint64_t)npix * p->samples_per_pixel;
+    c->stats.upload_ms = up;
+    c->stats.gather_ms = 0.0;
+    if (out8) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
+    if (outf) HIPCHK(c, hipMemcpyAsync(outf, c->d_f32, npix * 16, hipMemcpyDeviceToHost, c->stream));
+    if ((r = finish_frame(c)) != RRTE_OK) return r;
+    c->stats.frames++;
+    return RRTE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rrte_hip_abi_version(void) { return RRTE_ABI_VERSION; }
+
+rrte_status rrte_hip_create(int device, rrte_ctx** out) {
+    if (!out) return RRTE_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return RRTE_NO_DEVICE;
+    if (device < 0 || device >= n) return RRTE_NO_DEVICE;
+    rrte_ctx* c = new (std::nothrow) rrte_ctx();
+    if (!c) return RRTE_HIP_ERROR;
+    c->device = device;
+    auto bail = [&](hipError_t e) {
+        (void)e;
+        rrte_hip_destroy(c);
+        return RRTE_HIP_ERROR;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return bail(e);
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e);
+    if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail(e);
+    if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail(e);
+    if ((e = hipEventCreate(&c->ev2)) != hipSuccess) return bail(e);
+    if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), 2 * sizeof(unsigned long long))) != hipSuccess) return bail(e);
+    if ((e = hipMemset(c->d_counters, 0, 2 * sizeof(unsigned long long))) != hipSuccess) return bail(e);
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_counters), 2 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess) return bail(e);
+    c->h_counters[0] = c->h_counters[1] = 0;
+    *out = c;
+    return RRTE_OK;
+}
+
+void rrte_hip_destroy(rrte_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    void* bufs[] = {c->d_prims, c->d_mats, c->d_lights, c->d_nodes, c->d_rgba,
+                    c->d_f32,   c->d_counters, c->d_gather, c->d_full};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rrte_hip_last_error(const rrte_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+rrte_status rrte_hip_render(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out) {
+    if (!c) return RRTE_INVALID_ARG;
+    if (!out) return fail(c, RRTE_INVALID_ARG, "null output buffer");
+    return render_common(c, s, p, out, nullptr);
+}
+
+rrte_status rrte_hip_render_f32(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out8,
+                                float* outf) {
+    if (!c) return RRTE_INVALID_ARG;
+    return render_common(c, s, p, out8, outf);
+}
+
+rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, void* d_rgba,
+                                  void* d_f32, void* stream) {
+    if (!c) return RRTE_INVALID_ARG;
+    rrte_status r = validate(c, s, p);
+    if (r != RRTE_OK) return r;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    double up = 0.0;
+    if ((r = upload_scene(c, s, st, &up)) != RRTE_OK) return r;
+    const int nr = c->nranks, rk = c->rank;
+    c->nranks = 1;
+    c->rank = 0;
+    r = launch(c, s, p, p->height, static_cast<uint32_t*>(d_rgba), static_cast<float4*>(d_f32), st);
+    c->nranks = nr;
+    c->rank = rk;
+    if (r != RRTE_OK) return r;
+    c->pending_primary = (uint64_t)p->width * p->height * p->samples_per_pixel;
+    c->stats.upload_ms = up;
+    c->stats.frames++;
+    return RRTE_OK;
+}
+
+rrte_status rrte_hip_synchronize(rrte_ctx* c) {
+    if (!c) return RRTE_INVALID_ARG;
+    HIPCHK(c, hipDeviceSynchronize());
+    return finish_frame(c);
+}
+
+rrte_status rrte_hip_stats(rrte_ctx* c, rrte_stats* out) {
+    if (!c || !out) return RRTE_INVALID_ARG;
+    *out = c->stats;
+    return RRTE_OK;
+}
+
+uint32_t rrte_hip_band_rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank) {
+    return rows_for_rank(height, band_rows, nranks, rank);
+}
+
+rrte_status rrte_hip_comm_unique_id(uint8_t out_id[RRTE_UNIQUE_ID_BYTES]) {
+    if (!out_id) return RRTE_INVALID_ARG;
+    static_assert(sizeof(ncclUniqueId) == RRTE_UNIQUE_ID_BYTES, "unique id size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return RRTE_RCCL_ERROR;
+    memcpy(out_id, &id, sizeof id);
+    return RRTE_OK;
+}
+
+rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t id_bytes[RRTE_UNIQUE_ID_BYTES]) {
+    if (!c || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return fail(c, RRTE_INVALID_ARG, "bad comm args");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->comm) {
+        ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    ncclUniqueId id;
+    memcpy(&id, id_bytes, sizeof id);
+    NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return RRTE_OK;
+}
+
+rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
+                                         void* d_full, void* stream) {
+    if (!c) return RRTE_INVALID_ARG;
+    rrte_status r = validate(c, s, p);
+    if (r != RRTE_OK) return r;
+    if (root < 0 || root >= c->nranks) return fail(c, RRTE_INVALID_ARG, "root %d out of range", root);
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    double up = 0.0;
+    if ((r = upload_scene(c, s, st, &up)) != RRTE_OK) return r;
+    const uint32_t band = p->band_rows ? p->band_rows : 16;
+    rrte_render_params pp = *p;
+    pp.band_rows = band;
+    const uint32_t rows = rows_for_rank(p->height, band, c->nranks, c->rank);
+    const uint32_t cap = rows_for_rank(p->height, band, c->nranks, 0);  // rank 0 owns the most rows
+    const size_t slice = (size_t)cap * p->width;
+    if (c->nranks == 1) {
+        if (!d_full) return fail(c, RRTE_INVALID_ARG, "null output");
+        r = launch(c, s, p, p->height, static_cast<uint32_t*>(d_full), nullptr, st);
+        if (r == RRTE_OK) c->pending_primary = (uint64_t)p->width * p->height * p->samples_per_pixel;
+        return r;
+    }
+    if ((r = ensure(c, c->d_gather, c->cap_gather, slice * (size_t)c->nranks)) != RRTE_OK) return r;
+    uint32_t* mine = c->d_gather + (size_t)c->rank * slice;  // in-place send slot
+    if ((r = launch(c, s, &pp, rows, mine, nullptr, st)) != RRTE_OK) return r;
+    HIPCHK(c, hipEventRecord(c->ev1, st));
+    NCCLCHK(c, ncclGather(mine, c->d_gather, slice * 4, ncclUint8, root, c->comm, st));
+    if (c->rank == root) {
+        if (!d_full) return fail(c, RRTE_INVALID_ARG, "root needs an output buffer");
+        dim3 g((p->width + 255) / 256 < 8 ? (p->width + 255) / 256 : 8, p->height);
+        hipLaunchKernelGGL(deinterleave_kernel, g, dim3(256), 0, st, c->d_gather, static_cast<uint32_t*>(d_full),
+                           p->width, p->height, band, (uint32_t)c->nranks, cap);
+        HIPCHK(c, hipGetLastError());
+    }
+    c->pending_primary = (uint64_t)p->width * rows * p->samples_per_pixel;
+    c->stats.upload_ms = up;
+    c->stats.frames++;
+    return RRTE_OK;
+}
+
+rrte_status rrte_hip_render_gather(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
+                                   uint8_t* out) {
+    if (!c) return RRTE_INVALID_ARG;
+    rrte_status r = validate(c, s, p);
+    if (r != RRTE_OK) return r;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t npix = (size_t)p->width * p->height;
+    uint32_t* full = nullptr;
+    if (c->rank == root) {
+        if ((r = ensure(c, c->d_full, c->cap_full, npix)) != RRTE_OK) return r;
+        full = c->d_full;
+    }
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    if ((r = rrte_hip_render_gather_async(c, s, p, root, full, c->stream)) != RRTE_OK) return r;
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    if (c->rank == root && out) HIPCHK(c, hipMemcpyAsync(out, full, npix * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float k_ms = 0.0f, all_ms = 0.0f;
+    if (c->nranks > 1) {
+        (void)hipEventElapsedTime(&k_ms, c->ev0, c->ev1);
+        (void)hipEventElapsedTime(&all_ms, c->ev0, c->ev2);
+        c->stats.kernel_ms = k_ms;
+        c->stats.gather_ms = all_ms - k_ms;
+    }
+    return finish_frame(c);
+}
+
+}  // extern "C"
