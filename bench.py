@@ -1,0 +1,232 @@
+"""Benchmark: Mray/s (primary + shadow) of the sdf-showcase scene at 1920x1080.
+
+python bench.py --gpus N --steps K --warmup W
+  N = 1: one rrte_hip_render_async frame per step on cuda:0.
+  N > 1: launched by torch.distributed.run; every rank renders its interleaved
+         16-row bands of the SAME 1080p frame and the frame is gathered to rank 0
+         over RCCL/xGMI (rrte_hip_render_gather_async) -> strong scaling.
+A "step" is one frame.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from rrte_amd import LoweredScene, abi, scenes  # noqa: E402
+from rrte_amd.renderer import Context  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (packed)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scene", default="sdf-showcase", choices=sorted(scenes.SCENES))
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--mode", default="lambert_shadow", choices=["lambert_shadow", "refcompat"])
+    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, params, budget_s):
+    """The oracle (C restatement of Raytracer::render) on this host's cores, whole frames,
+    median over frames within the time budget (1 warm-up frame)."""
+    import oracle
+
+    threads = int(os.environ.get("RRTE_CPU_THREADS", os.cpu_count() or 1))
+    # the GPU box shows the whole machine in os.cpu_count(); our share is what sched_getaffinity allows
+    try:
+        threads = min(threads, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    oracle.render(scene, params, nthreads=threads, want_f32=False)  # warm-up
+    times, shadow = [], 0
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        _, _, shadow = oracle.render(scene, params, nthreads=threads, want_f32=False)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s or len(times) >= 25:
+            break
+    med = statistics.median(times)
+    rays = params.width * params.height * params.samples_per_pixel + shadow
+    return {
+        "value": rays / med / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
+        "sample": f"{len(times)} whole {params.width}x{params.height} frames of the same scene/mode, median "
+                  f"{med * 1e3:.1f} ms/frame, oracle/rrte_oracle.c -O3 -march=x86-64-v3, {threads} threads",
+    }
+
+
+def pmc_traffic(workload_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_*.json), or None."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("pmc_*.json")):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        if d.get("workload") == workload_key and d.get("hbm_bytes_per_launch") is not None:
+            best = d
+    return best
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+
+    dist_on = world > 1
+    if dist_on:
+        dist.init_process_group("gloo")  # control plane only; the frame gather is RCCL inside librrte_hip
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    objs, lights, cam, cfg = scenes.SCENES[args.scene](args.width, args.height, mode=args.mode)
+    cfg.band_rows = args.band_rows
+    scene = LoweredScene(objs, lights, cam)
+    prm = cfg.lower()
+    ctx = Context(local_rank)
+    lib = ctx.lib
+
+    if dist_on:
+        uid = torch.zeros(abi.UNIQUE_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            buf = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+            ctx.check(lib.rrte_hip_comm_unique_id(buf))
+            uid.copy_(torch.tensor(list(buf), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        idb = (C.c_uint8 * abi.UNIQUE_ID_BYTES)(*uid.tolist())
+        ctx.check(lib.rrte_hip_comm_init(ctx.h, world, rank, idb))
+
+    W, H = args.width, args.height
+    full = torch.empty(W * H, dtype=torch.int32, device=dev)
+    # a dedicated (non-null) stream: kernels, events and the gather all go on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sptr = C.c_void_p(stream.cuda_stream)
+    assert sptr.value, "need a non-null HIP stream handle"
+
+
+    def step():
+        if dist_on:
+            ctx.check(lib.rrte_hip_render_gather_async(ctx.h, scene.ref(), C.byref(prm), 0,
+                                                       full.data_ptr() if rank == 0 else None, sptr))
+        else:
+            ctx.check(lib.rrte_hip_render_async(ctx.h, scene.ref(), C.byref(prm), full.data_ptr(), None, sptr))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.check(lib.rrte_hip_synchronize(ctx.h))  # folds warm-up shadow counts away
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist_on:
+        dist.barrier()
+    ctx.check(lib.rrte_hip_synchronize(ctx.h))
+    st = ctx.stats()
+    elapsed = t1 - t0
+    launch_ms = [a.elapsed_time(b) for a, b in evs]
+    rows = lib.rrte_hip_band_rows_for_rank(H, args.band_rows, world, rank) if dist_on else H
+    primary = W * rows * prm.samples_per_pixel * args.steps
+    shadow = int(st.shadow_rays)
+
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        cnt = torch.tensor([primary, shadow], dtype=torch.float64)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        primary, shadow = int(cnt[0].item()), int(cnt[1].item())
+
+    if rank == 0:
+        rays = primary + shadow
+        value = rays / elapsed / 1e6
+        avg_launch_ms = float(np.mean(launch_ms))
+        # algorithmic HBM bytes per launch: the RGBA8 framebuffer store, 4 B per pixel;
+        # the scene (<= a few KB) is served from the scalar cache and counts once.
+        bytes_per_launch = 4 * W * H
+        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+        wl = f"{args.scene}@{W}x{H}/{args.mode}"
+        pmc = pmc_traffic(wl)
+        line = {
+            "metric": "Mray/s (primary+shadow) at 1920x1080, sdf-showcase scene; 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong" if world > 1 else "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.scene} {W}x{H}, {args.mode}, spp=1, pixel-centre jitter"
+                            + (f", {args.band_rows}-row bands interleaved over {world} GPUs + RCCL gather to rank 0"
+                               if world > 1 else ""),
+                "scene": args.scene, "width": W, "height": H, "mode": args.mode,
+                "primary_rays_per_frame": W * H * prm.samples_per_pixel,
+                "shadow_rays_per_frame": shadow // args.steps,
+                "parallelism": f"rows{world}" if world > 1 else "single",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 3),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                "kernel": "rrte::ray_kernel<LAMBERT_SHADOW>" if args.mode == "lambert_shadow" else "rrte::ray_kernel<REFCOMPAT>",
+                "avg_launch_ms": round(avg_launch_ms, 5),
+                "bytes_per_launch": bytes_per_launch,
+                "note": "VALU-bound path (no dense contraction, no MFMA); HBM traffic is the 4 B/pixel frame store",
+            },
+        }
+        if pmc and pmc.get("valu") is not None:
+            line["valu"] = pmc["valu"]
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(scene, prm, args.cpu_seconds)
+            line["cpu_baseline"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 2)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -127,6 +127,13 @@ def load() -> C.CDLL:
         raise RuntimeError(
             f"librrte_hip.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
+    # torch-rocm bundles its own libamdhip64.so.7 / librccl.so.1 (same SONAMEs as /opt/rocm).
+    # Two HIP runtimes in one process corrupt each other at exit, so if torch is installed it is
+    # loaded first and librrte_hip.so binds to the runtime torch already mapped (one per process).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(lib, name)

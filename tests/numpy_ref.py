@@ -1,0 +1,404 @@
+"""Independent numpy float32 restatement of the reference ray loop — TEST ONLY.
+
+Vectorised over pixels; every op is an elementwise float32 numpy op (IEEE, one
+rounding, no FMA), so it must agree bit-for-bit with oracle/rrte_oracle.c on
+the same inputs.  It restates (paths relative to Melthizar/RRTE):
+  raytracer.rs:45-148 (render/ray_color, REFCOMPAT depth 1), camera.rs:98-117,
+  primitives.rs:57-725 (all seven intersectors), light.rs:170-194, color.rs:48-113,
+and the build-defined LAMBERT_SHADOW pass and SDF leaf/CSG formulas.
+It is written from the reference source, not from the C oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from rrte_amd import abi
+
+F = np.float32
+INF = F(np.inf)
+
+
+def _v(a):
+    return np.asarray(a, dtype=np.float32)
+
+
+def dot(a, b):
+    return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]
+
+
+def normalize(a):
+    r = F(1.0) / np.sqrt(dot(a, a))
+    return [a[0] * r, a[1] * r, a[2] * r]
+
+
+def cross(a, b):
+    return [a[1] * b[2] - b[1] * a[2], a[2] * b[0] - b[2] * a[0], a[0] * b[1] - b[0] * a[1]]
+
+
+def at(o, d, t):
+    return [o[0] + d[0] * t, o[1] + d[1] * t, o[2] + d[2] * t]
+
+
+def quat_rotate(q, v):
+    b = [F(q[0]), F(q[1]), F(q[2])]
+    w = F(q[3])
+    k0 = w * w - ((b[0] * b[0] + b[1] * b[1]) + b[2] * b[2])
+    k1 = dot(v, b) * F(2.0)
+    k2 = w * F(2.0)
+    c = cross(b, v)
+    return [(v[i] * k0 + b[i] * k1) + c[i] * k2 for i in range(3)]
+
+
+def mat4_srt(trs):
+    x, y, z, w = (F(t) for t in trs[3:7])
+    x2, y2, z2 = x + x, y + y, z + z
+    xx, xy, xz, yy, yz, zz = x * x2, x * y2, x * z2, y * y2, y * z2, z * z2
+    wx, wy, wz = w * x2, w * y2, w * z2
+    s = [F(t) for t in trs[7:10]]
+    cols = [[F(1) - (yy + zz), xy + wz, xz - wy], [xy - wz, F(1) - (xx + zz), yz + wx],
+            [xz + wy, yz - wx, F(1) - (xx + yy)]]
+    m = np.zeros(16, np.float32)
+    for c in range(3):
+        for r in range(3):
+            m[c * 4 + r] = cols[c][r] * s[c]
+        m[c * 4 + 3] = F(0) * s[c]
+    m[12:15] = [F(t) for t in trs[0:3]]
+    m[15] = F(1)
+    return m
+
+
+def mat4_inverse(m):
+    M = lambda c, r: m[c * 4 + r]  # noqa: E731
+    c = {}
+    c[0] = M(2, 2) * M(3, 3) - M(3, 2) * M(2, 3); c[2] = M(1, 2) * M(3, 3) - M(3, 2) * M(1, 3)
+    c[3] = M(1, 2) * M(2, 3) - M(2, 2) * M(1, 3); c[4] = M(2, 1) * M(3, 3) - M(3, 1) * M(2, 3)
+    c[6] = M(1, 1) * M(3, 3) - M(3, 1) * M(1, 3); c[7] = M(1, 1) * M(2, 3) - M(2, 1) * M(1, 3)
+    c[8] = M(2, 1) * M(3, 2) - M(3, 1) * M(2, 2); c[10] = M(1, 1) * M(3, 2) - M(3, 1) * M(1, 2)
+    c[11] = M(1, 1) * M(2, 2) - M(2, 1) * M(1, 2); c[12] = M(2, 0) * M(3, 3) - M(3, 0) * M(2, 3)
+    c[14] = M(1, 0) * M(3, 3) - M(3, 0) * M(1, 3); c[15] = M(1, 0) * M(2, 3) - M(2, 0) * M(1, 3)
+    c[16] = M(2, 0) * M(3, 2) - M(3, 0) * M(2, 2); c[18] = M(1, 0) * M(3, 2) - M(3, 0) * M(1, 2)
+    c[19] = M(1, 0) * M(2, 2) - M(2, 0) * M(1, 2); c[20] = M(2, 0) * M(3, 1) - M(3, 0) * M(2, 1)
+    c[22] = M(1, 0) * M(3, 1) - M(3, 0) * M(1, 1); c[23] = M(1, 0) * M(2, 1) - M(2, 0) * M(1, 1)
+    fac = [[c[0], c[0], c[2], c[3]], [c[4], c[4], c[6], c[7]], [c[8], c[8], c[10], c[11]],
+           [c[12], c[12], c[14], c[15]], [c[16], c[16], c[18], c[19]], [c[20], c[20], c[22], c[23]]]
+    vec = [[M(1, 0), M(0, 0), M(0, 0), M(0, 0)], [M(1, 1), M(0, 1), M(0, 1), M(0, 1)],
+           [M(1, 2), M(0, 2), M(0, 2), M(0, 2)], [M(1, 3), M(0, 3), M(0, 3), M(0, 3)]]
+    inv = np.zeros(16, np.float32)
+    for i in range(4):
+        sa = F(-1) if i & 1 else F(1)
+        sb = -sa
+        inv[0 + i] = ((vec[1][i] * fac[0][i] - vec[2][i] * fac[1][i]) + vec[3][i] * fac[2][i]) * sa
+        inv[4 + i] = ((vec[0][i] * fac[0][i] - vec[2][i] * fac[3][i]) + vec[3][i] * fac[4][i]) * sb
+        inv[8 + i] = ((vec[0][i] * fac[1][i] - vec[1][i] * fac[3][i]) + vec[3][i] * fac[5][i]) * sa
+        inv[12 + i] = ((vec[0][i] * fac[2][i] - vec[1][i] * fac[4][i]) + vec[2][i] * fac[5][i]) * sb
+    det = (M(0, 0) * inv[0] + M(0, 1) * inv[4]) + (M(0, 2) * inv[8] + M(0, 3) * inv[12])
+    return inv * (F(1) / det)
+
+
+def m_point(m, p):
+    return [((m[0 + r] * p[0] + m[4 + r] * p[1]) + m[8 + r] * p[2]) + m[12 + r] for r in range(3)]
+
+
+def m_vector(m, p):
+    return [(m[0 + r] * p[0] + m[4 + r] * p[1]) + m[8 + r] * p[2] for r in range(3)]
+
+
+class Hits:
+    """Per-ray hit record arrays (t, p, n, valid)."""
+
+    def __init__(self, n):
+        self.t = np.full(n, np.inf, np.float32)
+        self.p = [np.zeros(n, np.float32) for _ in range(3)]
+        self.n = [np.zeros(n, np.float32) for _ in range(3)]
+        self.ok = np.zeros(n, bool)
+
+    def set(self, mask, t, p, outward, d):
+        front = dot(d, outward) < F(0)
+        nn = [np.where(front, outward[k], -outward[k]) for k in range(3)]
+        self.t = np.where(mask, t, self.t)
+        for k in range(3):
+            self.p[k] = np.where(mask, p[k], self.p[k])
+            self.n[k] = np.where(mask, nn[k], self.n[k])
+        self.ok |= mask
+
+
+def _local(pr, o, d):
+    m = mat4_srt(list(pr.trs))
+    inv = mat4_inverse(m)
+    lo = m_point(inv, o)
+    ld = normalize(normalize(m_vector(inv, d)))
+    return m, lo, ld
+
+
+def intersect(pr, o, d, tmin, tmax):
+    """SceneObject::intersect for one prim over all rays; returns a Hits record."""
+    n = o[0].shape[0]
+    h = Hits(n)
+    p = [F(v) for v in pr.p]
+    with np.errstate(all="ignore"):
+        if pr.kind == abi.PRIM_SPHERE:
+            c = p[0:3]
+            oc = [o[k] - c[k] for k in range(3)]
+            a = dot(d, d)
+            hb = dot(oc, d)
+            cc = dot(oc, oc) - p[3] * p[3]
+            disc = hb * hb - a * cc
+            ok = disc >= F(0)
+            sq = np.sqrt(np.where(ok, disc, F(0)))
+            r1 = (-hb - sq) / a
+            r2 = (-hb + sq) / a
+            bad1 = (r1 < tmin) | (tmax < r1)
+            root = np.where(bad1, r2, r1)
+            ok &= ~(bad1 & ((r2 < tmin) | (tmax < r2)))
+            pt = at(o, d, root)
+            h.set(ok, root, pt, [(pt[k] - c[k]) / p[3] for k in range(3)], d)
+        elif pr.kind == abi.PRIM_PLANE:
+            pt0, nrm = p[0:3], p[4:7]
+            denom = dot(nrm, d)
+            t = dot([pt0[k] - o[k] for k in range(3)], nrm) / denom
+            ok = ~(np.abs(denom) < F(1e-6)) & ~((t < tmin) | (t > tmax))
+            pt = at(o, d, t)
+            out = [np.where(denom < F(0), nrm[k], -nrm[k]) for k in range(3)]
+            h.set(ok, t, pt, out, d)
+        elif pr.kind == abi.PRIM_CUBE:
+            m, lo, ld = _local(pr, o, d)
+            half = [p[4 + k] * F(0.5) for k in range(3)]
+            mn_ = [p[k] - half[k] for k in range(3)]
+            mx_ = [p[k] + half[k] for k in range(3)]
+            tn = np.full(n, tmin, np.float32)
+            tf = np.full(n, tmax, np.float32)
+            nrm = [np.zeros(n, np.float32) for _ in range(3)]
+            alive = np.ones(n, bool)
+            for i in range(3):
+                ax = [F(1) if k == i else F(0) for k in range(3)]
+                oc, dc = dot(lo, ax), dot(ld, ax)
+                loi, hii = dot(mn_, ax), dot(mx_, ax)
+                par = np.abs(dc) < F(1e-6)
+                alive &= ~(par & ((oc < loi) | (oc > hii)))
+                t1, t2 = (loi - oc) / dc, (hii - oc) / dc
+                lt = t1 < t2
+                tsn, tsf = np.where(lt, t1, t2), np.where(lt, t2, t1)
+                upd = ~par & (tsn > tn)
+                tn = np.where(upd, tsn, tn)
+                for k in range(3):
+                    nrm[k] = np.where(upd, np.where(lt, -ax[k], ax[k]), nrm[k])
+                tf = np.where(~par & (tsf < tf), tsf, tf)
+                alive &= ~(~par & (tn > tf))
+            t = np.where(tn >= tmin, tn, tf)
+            ok = alive & ~((t < tmin) | (t > tmax))
+            lp = at(lo, ld, t)
+            h.set(ok, t, m_point(m, lp), normalize(m_vector(m, nrm)), d)
+        elif pr.kind in (abi.PRIM_CYLINDER, abi.PRIM_CONE):
+            m, lo, ld = _local(pr, o, d)
+            c, rad, ht = p[0:3], p[3], p[4]
+            hh = ht * F(0.5)
+            oc = [lo[k] - c[k] for k in range(3)]
+            if pr.kind == abi.PRIM_CYLINDER:
+                a = ld[0] * ld[0] + ld[2] * ld[2]
+                b = F(2) * (oc[0] * ld[0] + oc[2] * ld[2])
+                cc = oc[0] * oc[0] + oc[2] * oc[2] - rad * rad
+            else:
+                k = rad / ht
+                k2 = k * k
+                a = ld[0] * ld[0] + ld[2] * ld[2] - k2 * ld[1] * ld[1]
+                b = F(2) * (oc[0] * ld[0] + oc[2] * ld[2] - k2 * (oc[1] - hh) * ld[1])
+                cc = oc[0] * oc[0] + oc[2] * oc[2] - k2 * (oc[1] - hh) * (oc[1] - hh)
+            disc = b * b - F(4) * a * cc
+            ok0 = disc >= F(0)
+            sq = np.sqrt(np.where(ok0, disc, F(0)))
+            done = ~ok0
+            for t in ((-b - sq) / (F(2) * a), (-b + sq) / (F(2) * a)):
+                pt = at(lo, ld, t)
+                inr = (t >= tmin) & (t <= tmax)
+                if pr.kind == abi.PRIM_CYLINDER:
+                    iny = np.abs(pt[1] - c[1]) <= hh
+                    ln = [(pt[0] - c[0]) / rad, np.zeros(n, np.float32), (pt[2] - c[2]) / rad]
+                else:
+                    yl = pt[1] - c[1]
+                    iny = (yl >= -hh) & (yl <= hh)
+                    rr = np.sqrt(pt[0] * pt[0] + pt[2] * pt[2])
+                    ln = normalize([pt[0] / rr, np.full(n, k, np.float32), pt[2] / rr])
+                sel = ~done & inr & iny
+                h.set(sel, t, m_point(m, pt), normalize(m_vector(m, ln)), d)
+                done |= sel
+        elif pr.kind == abi.PRIM_CAPSULE:
+            m, lo, ld = _local(pr, o, d)
+            c, rad, hh = p[0:3], p[3], p[4] * F(0.5)
+            closest = np.full(n, np.inf, np.float32)
+            a = dot(ld, ld)
+            for cap in (0, 1):
+                cen = [c[0], c[1] + hh, c[2]] if cap == 0 else [c[0], c[1] - hh, c[2]]
+                oc = [lo[k] - cen[k] for k in range(3)]
+                hb = dot(oc, ld)
+                cc = dot(oc, oc) - rad * rad
+                disc = hb * hb - a * cc
+                ok0 = disc >= F(0)
+                sq = np.sqrt(np.where(ok0, disc, F(0)))
+                for t in ((-hb - sq) / a, (-hb + sq) / a):
+                    pt = at(lo, ld, t)
+                    side = (pt[1] >= c[1]) if cap == 0 else (pt[1] <= c[1])
+                    sel = ok0 & (t >= tmin) & (t <= tmax) & (t < closest) & side
+                    ln = normalize([pt[k] - cen[k] for k in range(3)])
+                    h.set(sel, t, m_point(m, pt), normalize(m_vector(m, ln)), d)
+                    closest = np.where(sel, t, closest)
+            oc = [lo[k] - c[k] for k in range(3)]
+            ac = ld[0] * ld[0] + ld[2] * ld[2]
+            bc = F(2) * (oc[0] * ld[0] + oc[2] * ld[2])
+            cy = oc[0] * oc[0] + oc[2] * oc[2] - rad * rad
+            disc = bc * bc - F(4) * ac * cy
+            ok0 = disc >= F(0)
+            sq = np.sqrt(np.where(ok0, disc, F(0)))
+            for t in ((-bc - sq) / (F(2) * ac), (-bc + sq) / (F(2) * ac)):
+                pt = at(lo, ld, t)
+                sel = ok0 & (t >= tmin) & (t <= tmax) & (t < closest) & (np.abs(pt[1] - c[1]) <= hh)
+                ln = [(pt[0] - c[0]) / rad, np.zeros(n, np.float32), (pt[2] - c[2]) / rad]
+                h.set(sel, t, m_point(m, pt), normalize(m_vector(m, ln)), d)
+                closest = np.where(sel, t, closest)
+        elif pr.kind == abi.PRIM_TRIANGLE:
+            v0, v1, v2 = p[0:3], p[3:6], p[6:9]
+            e1 = [v1[k] - v0[k] for k in range(3)]
+            e2 = [v2[k] - v0[k] for k in range(3)]
+            hh = cross(d, [np.full(n, e2[k], np.float32) for k in range(3)])
+            a = dot(e1, hh)
+            f = F(1) / a
+            s = [o[k] - v0[k] for k in range(3)]
+            u = f * dot(s, hh)
+            q = cross(s, [np.full(n, e1[k], np.float32) for k in range(3)])
+            v = f * dot(d, q)
+            t = f * dot(e2, q)
+            ok = ~((a > F(-1e-6)) & (a < F(1e-6))) & ~((u < F(0)) | (u > F(1))) & ~((v < F(0)) | (u + v > F(1)))
+            ok &= ~((t < tmin) | (t > tmax))
+            w = F(1) - u - v
+            nn = normalize([(p[9 + k] * w + p[12 + k] * u) + p[15 + k] * v for k in range(3)])
+            h.set(ok, t, at(o, d, t), nn, d)
+        else:
+            raise NotImplementedError(pr.kind)
+    return h
+
+
+def render(scene: "abi.SceneIR", params: "abi.RenderParams"):
+    """REFCOMPAT (max_depth 1) or LAMBERT_SHADOW with analytic prims and point lights,
+    pixel-centre jitter, spp 1.  Returns (rgba8 HxWx4, f32 HxWx4, shadow_rays)."""
+    W, H = params.width, params.height
+    assert params.samples_per_pixel == 1 and params.jitter == abi.JITTER_CENTER
+    ys, xs = np.mgrid[0:H, 0:W]
+    u = (xs.ravel().astype(np.float32) + F(0.5)) / F(W)
+    v = (ys.ravel().astype(np.float32) + F(0.5)) / F(H)
+    cam = scene.camera
+    ndx = F(2) * u - F(1)
+    ndy = F(1) - F(2) * v
+    hh = np.tan(F(cam.fov) * F(0.5))
+    hw = F(cam.aspect_ratio) * hh
+    cd = normalize([ndx * hw, ndy * hh, np.full_like(u, F(-1))])
+    d = normalize(quat_rotate(list(cam.rotation), cd))
+    n = u.shape[0]
+    o = [np.full(n, F(cam.position[k]), np.float32) for k in range(3)]
+    prims = [scene.prims[i] for i in range(scene.num_prims)]
+    best = Hits(n)
+    idx = np.full(n, -1)
+    for i, pr in enumerate(prims):
+        h = intersect(pr, o, d, F(params.t_min), INF)
+        better = h.ok & (~best.ok | (h.t < best.t))
+        best.t = np.where(better, h.t, best.t)
+        for k in range(3):
+            best.p[k] = np.where(better, h.p[k], best.p[k])
+            best.n[k] = np.where(better, h.n[k], best.n[k])
+        best.ok |= better
+        idx = np.where(better, i, idx)
+    col = [np.zeros(n, np.float32) for _ in range(4)]
+    shadow = 0
+    bg = [F(c) for c in params.background]
+    mats = [scene.materials[i] for i in range(scene.num_materials)]
+    lights = [scene.lights[i] for i in range(scene.num_lights)]
+    hit = best.ok
+    matidx = np.array([prims[i].material if i >= 0 else -1 for i in idx])
+    with np.errstate(all="ignore"):
+        alb = [np.array([F(mats[m].albedo[k]) if m >= 0 else F(0) for m in matidx], np.float32) for k in range(4)]
+        for k in range(4):
+            col[k] = np.where(hit, (F(0) if k < 3 else F(1)) + (alb[k] * F(0.1)) * F(0.1), bg[k])
+        for li, l in enumerate(lights):
+            assert l.kind == abi.LIGHT_POINT
+            lv = [F(l.position[k]) - best.p[k] for k in range(3)]
+            dist = np.sqrt(dot(lv, lv))
+            ldir = normalize(lv)
+            att = F(1) / ((F(1) + F(l.linear) * dist) + (F(l.quadratic) * dist) * dist)
+            att = np.where(dist > F(l.range), F(0), np.maximum(att, F(0)))
+            cI = [F(l.color[k]) * F(l.intensity) for k in range(4)]
+            if params.mode == abi.MODE_REFCOMPAT:
+                for k in range(4):
+                    col[k] = np.where(hit, col[k] + cI[k] * att, col[k])
+            else:
+                ndl = dot(best.n, ldir)
+                cast = hit & (ndl > F(0)) & (att > F(0))
+                shadow += int(cast.sum())
+                bias = F(params.shadow_bias)
+                so = normalize(ldir)
+                sorg = [best.p[k] + best.n[k] * bias for k in range(3)]
+                occ = np.zeros(n, bool)
+                for pr in prims:
+                    hs = intersect(pr, sorg, so, bias, dist)
+                    occ |= hs.ok
+                lit = cast & ~occ
+                fct = att * ndl
+                for k in range(3):
+                    col[k] = np.where(lit, col[k] + alb[k] * (cI[k] * fct), col[k])
+        if params.mode == abi.MODE_REFCOMPAT:
+            # scatter -> ray_color(depth 0) = BLACK adds Color::from(albedo * 0) with alpha 1
+            col[3] = np.where(hit, col[3] + F(1), col[3])
+        no_mat = hit & (matidx < 0)
+        for k in range(4):
+            col[k] = np.where(no_mat, F(0) if k < 3 else F(1), col[k])
+        # render(): color = BLACK + sample (alpha starts at 1), then * (1/spp) (raytracer.rs:64-76)
+        col = [(F(0) if k < 3 else F(1)) + col[k] for k in range(4)]
+        col = [c * F(1.0) for c in col]
+        inv_g = F(1) / F(params.gamma)
+        g = [np.power(col[k], inv_g) if k < 3 else col[k] for k in range(4)]
+        g = [np.where(np.isnan(x), x, np.clip(x, F(0), F(1))) for x in g]
+        q = []
+        for x in g:
+            y = x * F(255)
+            q.append(np.where(~(y > F(0)), 0, np.where(y >= F(255), 255, np.nan_to_num(y).astype(np.int64))))
+    rgba8 = np.stack(q, -1).astype(np.uint8).reshape(H, W, 4)
+    f32 = np.stack(g, -1).reshape(H, W, 4)
+    return rgba8, f32, shadow
+
+
+# ------------------------------------------------------------ SDF formulas
+def sdf_leaf(op, f, p):
+    f = [F(x) for x in f]
+    q = [p[k] - f[k] for k in range(3)]
+    l2 = lambda a, b: np.sqrt(a * a + b * b)  # noqa: E731
+    l3 = lambda a, b, c: np.sqrt((a * a + b * b) + c * c)  # noqa: E731
+    mx = lambda a, b: np.where(b > a, b, a)  # noqa: E731
+    mn = lambda a, b: np.where(b < a, b, a)  # noqa: E731
+    Z = F(0)
+    if op == abi.SDF_SPHERE:
+        return l3(*q) - f[3]
+    if op == abi.SDF_BOX:
+        dx, dy, dz = np.abs(q[0]) - f[4] * F(.5), np.abs(q[1]) - f[5] * F(.5), np.abs(q[2]) - f[6] * F(.5)
+        return l3(mx(dx, Z), mx(dy, Z), mx(dz, Z)) + mn(mx(dx, mx(dy, dz)), Z)
+    if op == abi.SDF_CYLINDER:
+        dx, dy = l2(q[0], q[2]) - f[3], np.abs(q[1]) - f[4] * F(.5)
+        return mn(mx(dx, dy), Z) + l2(mx(dx, Z), mx(dy, Z))
+    if op == abi.SDF_TORUS:
+        return l2(l2(q[0], q[2]) - f[3], q[1]) - f[4]
+    if op == abi.SDF_RING:
+        return l2(l2(q[0], q[1]) - f[3], q[2]) - f[4]
+    if op == abi.SDF_CAPSULE:
+        hh = f[4] * F(.5)
+        y = q[1] - mn(mx(q[1], -hh), hh)
+        return l3(q[0], y, q[2]) - f[3]
+    if op == abi.SDF_TUBE:
+        rad = l2(q[0], q[2])
+        mid, half = (f[3] + f[4]) * F(.5), (f[3] - f[4]) * F(.5)
+        dx, dy = np.abs(rad - mid) - half, np.abs(q[1]) - f[5] * F(.5)
+        return mn(mx(dx, dy), Z) + l2(mx(dx, Z), mx(dy, Z))
+    raise NotImplementedError(op)
+
+
+def smin(a, b, k):
+    k = F(k)
+    h = (F(0.5) + (F(0.5) * (b - a)) / k)
+    h = np.where(F(1) < np.where(F(0) > h, F(0), h), F(1), np.where(F(0) > h, F(0), h))
+    om = F(1) - h
+    return (a * h + b * om) - (k * h) * om

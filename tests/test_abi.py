@@ -1,0 +1,74 @@
+"""The C-ABI boundary (include/rrte_hip.h): the library loads, exports every declared
+entry point, struct layouts match, and host-side argument checks work without a GPU."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from rrte_amd import abi
+
+HEADER = Path(__file__).resolve().parents[1] / "include" / "rrte_hip.h"
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(rrte_hip_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = abi.load()
+    names = declared_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in abi.EXPORTS, f"{n} missing from the ctypes mirror"
+    assert lib.rrte_hip_abi_version() == 1
+
+
+def test_struct_layouts_match_header_comments():
+    assert C.sizeof(abi.Prim) == 192
+    assert C.sizeof(abi.Material) == 32
+    assert C.sizeof(abi.Light) == 80
+    assert C.sizeof(abi.SdfNode) == 64
+    assert C.sizeof(abi.Camera) == 80
+    assert C.sizeof(abi.RenderParams) == 64
+    text = HEADER.read_text()
+    for name, size in [("rrte_material", 32), ("rrte_light", 80), ("rrte_sdf_node", 64), ("rrte_camera", 80),
+                       ("rrte_render_params", 64)]:
+        assert re.search(r"\}\s*" + name + r";\s*/\*\s*" + str(size) + " bytes", text), name
+
+
+def test_null_arguments_are_rejected_without_a_device():
+    lib = abi.load()
+    assert lib.rrte_hip_create(0, None) == abi.RRTE_INVALID_ARG
+    assert lib.rrte_hip_render(None, None, None, None) == abi.RRTE_INVALID_ARG
+    assert lib.rrte_hip_stats(None, None) == abi.RRTE_INVALID_ARG
+    assert lib.rrte_hip_comm_unique_id(None) == abi.RRTE_INVALID_ARG
+    assert lib.rrte_hip_last_error(None) == b"null context"
+    lib.rrte_hip_destroy(None)  # no-op
+
+
+def test_create_reports_no_device_off_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    h = C.c_void_p()
+    assert abi.load().rrte_hip_create(0, C.byref(h)) == abi.RRTE_NO_DEVICE
+
+
+@pytest.mark.parametrize("H,band,n", [(1080, 16, 2), (1080, 16, 8), (2160, 16, 8), (1000, 16, 3), (7, 16, 4),
+                                      (1080, 1, 8), (1, 16, 1)])
+def test_band_partition_covers_every_row_once(H, band, n):
+    lib = abi.load()
+    rows = [lib.rrte_hip_band_rows_for_rank(H, band, n, r) for r in range(n)]
+    assert sum(rows) == H
+    assert rows[0] == max(rows)  # rank 0 owns the most rows: the gather slot size
+    # mirror of the device mapping image_row(): local row -> image row, a bijection onto [0, H)
+    seen = []
+    for r in range(n):
+        for lr in range(rows[r]):
+            b, w = divmod(lr, band)
+            seen.append((b * n + r) * band + w if n > 1 else lr)
+    assert sorted(seen) == list(range(H))
