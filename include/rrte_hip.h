@@ -29,8 +29,10 @@
 #ifndef RRTE_HIP_H
 #define RRTE_HIP_H
 
+#ifndef __HIPCC_RTC__ /* hiprtc (scene-specialised kernels) provides the fixed-width types itself */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -232,6 +234,9 @@ typedef struct rrte_stats {
     double gather_ms;        /* RCCL gather + de-interleave time               */
     double upload_ms;        /* scene H2D time (0 when the scene was cached)   */
     uint64_t frames;         /* frames rendered by this context                */
+    uint32_t jit_active;     /* 1 if the last frame ran a scene-specialised kernel */
+    uint32_t _pad0;
+    double jit_compile_ms;   /* hiprtc compile time of the last specialised kernel */
 } rrte_stats;
 
 typedef struct rrte_ctx rrte_ctx;
@@ -265,6 +270,16 @@ rrte_status rrte_hip_render_async(rrte_ctx* ctx, const rrte_scene_ir* scene,
 rrte_status rrte_hip_synchronize(rrte_ctx* ctx);
 
 rrte_status rrte_hip_stats(rrte_ctx* ctx, rrte_stats* out);
+
+/* Scene-specialised kernels (hiprtc).  OFF: always the
+ * generic kernel.  ON: specialise a scene on its first frame.  AUTO (default):
+ * specialise once the same scene is rendered a second time.  Results are
+ * bit-identical either way; env RRTE_JIT=0/1/2 overrides the default. */
+typedef enum rrte_jit_mode { RRTE_JIT_OFF = 0, RRTE_JIT_ON = 1, RRTE_JIT_AUTO = 2 } rrte_jit_mode;
+rrte_status rrte_hip_set_jit(rrte_ctx* ctx, int mode);
+/* Diagnostic: generate + hiprtc-compile the specialised kernel for `scene`
+ * (no device needed).  RRTE_OK if it compiles; otherwise the log is copied out. */
+rrte_status rrte_hip_jit_check(const rrte_scene_ir* scene, int mode, char* log, size_t log_len);
 
 /* ----------------------------------------------------- multi-GPU (RCCL/xGMI) */
 /* Row-band partition: band b (band_rows rows) belongs to rank b % nranks.

@@ -32,6 +32,7 @@ SDF_BEND, SDF_TWIST, SDF_TAPER, SDF_NOISE, SDF_WAVE = 64, 65, 66, 67, 68
 SDF_POP_POINT = 96
 SDF_MAX_STACK, SDF_MAX_POINT_STACK, SDF_MAX_OCTAVES = 8, 4, 8
 UNIQUE_ID_BYTES = 128
+JIT_OFF, JIT_ON, JIT_AUTO = 0, 1, 2
 
 
 # --------------------------------------------------------------- structs
@@ -90,7 +91,8 @@ class SceneIR(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("kernel_ms", C.c_double),
-                ("gather_ms", C.c_double), ("upload_ms", C.c_double), ("frames", C.c_uint64)]
+                ("gather_ms", C.c_double), ("upload_ms", C.c_double), ("frames", C.c_uint64),
+                ("jit_active", C.c_uint32), ("_pad0", C.c_uint32), ("jit_compile_ms", C.c_double)]
 
 
 assert C.sizeof(Prim) == 192 and C.sizeof(Material) == 32 and C.sizeof(Light) == 80
@@ -108,6 +110,8 @@ EXPORTS = {
     "rrte_hip_render_async": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), _P, _P, _P]),
     "rrte_hip_synchronize": (C.c_int, [_P]),
     "rrte_hip_stats": (C.c_int, [_P, C.POINTER(Stats)]),
+    "rrte_hip_set_jit": (C.c_int, [_P, C.c_int]),
+    "rrte_hip_jit_check": (C.c_int, [C.POINTER(SceneIR), C.c_int, C.c_char_p, C.c_size_t]),
     "rrte_hip_comm_unique_id": (C.c_int, [_P]),
     "rrte_hip_comm_init": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "rrte_hip_render_gather": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_int, _P]),

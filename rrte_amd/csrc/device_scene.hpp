@@ -6,8 +6,10 @@
 // HIP default correctly-rounded f32 divide/sqrt.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "../../include/rrte_hip.h"
 
@@ -73,6 +75,7 @@ struct KParams {
     float half_h, aspect;
     float ortho_l, ortho_r, ortho_b, ortho_t;
     float cam_xf[12];
+    uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
 };
 
 // ---------------------------------------------------------------- f32 vec3

@@ -1,0 +1,32 @@
+// jit.hpp — scene-specialised kernel compilation (see jit.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "device_scene.hpp"
+
+namespace rrte {
+
+struct JitKernel {
+    hipModule_t module = nullptr;
+    hipFunction_t fn = nullptr;
+    double compile_ms = 0.0;
+    size_t code_bytes = 0;
+};
+
+// HIP source for one scene + shading mode: the scene as static constexpr arrays
+// and an extern "C" rrte_jit_kernel instantiating ray_kernel_body<mode, Scene>.
+std::string jit_source(const DPrim* prims, uint32_t np, const DMaterial* mats, uint32_t nm, const DLight* lights,
+                       uint32_t nl, const rrte_sdf_node* nodes, uint32_t nn, int mode);
+
+// hiprtc compile for gfx950 + module load.  On failure `log` holds the reason.
+bool jit_compile(const std::string& src, JitKernel& out, std::string& log);
+
+void jit_release(JitKernel& k);
+
+// hiprtc compile only (no module load, no device needed): diagnostics / CPU tests.
+bool jit_compile_only(const std::string& src, std::string& log);
+
+}  // namespace rrte

@@ -14,13 +14,71 @@ namespace rrte {
 
 constexpr float kInf = __builtin_huge_valf();
 
+// Runtime scene: device pointers + counts (the generic kernel).  A
+// scene-specialised kernel (jit.cpp, hiprtc) instead passes a struct whose
+// members are static constexpr arrays and counts: the same device code below
+// then fully unrolls its object / node / light loops and folds every scene
+// constant into the instruction stream.
 struct SceneView {
+    static constexpr bool kStatic = false;
     const DPrim* __restrict__ prims;
     const DMaterial* __restrict__ mats;
     const DLight* __restrict__ lights;
     const rrte_sdf_node* __restrict__ nodes;
     uint32_t num_prims, num_lights, num_materials;
 };
+
+// Loop over objects / lights: a plain loop for the runtime scene, compile-time
+// recursion (every index a constant) for a static scene, so that the object's
+// record, kind and SDF program fold into the code.
+template <uint32_t V>
+struct UC {
+    static constexpr uint32_t value = V;
+    __device__ __forceinline__ constexpr operator uint32_t() const { return V; }
+};
+template <uint32_t I, uint32_t N, class F>
+__device__ __forceinline__ void static_for(F& f) {
+    if constexpr (I < N) {
+        f(UC<I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+template <class S, class F>
+__device__ __forceinline__ void for_each_prim(const S& sc, F&& f) {
+    if constexpr (S::kStatic) {
+        static_for<0, S::num_prims>(f);
+    } else {
+        for (uint32_t i = 0; i < sc.num_prims; ++i) f(i);
+    }
+}
+// Scene record accessors.  For a static scene the record is copied in a
+// constant-expression context (constexpr local): device-side copies of
+// constexpr globals may be emitted as externally-initialised memory whose
+// loads do not fold, while a constexpr copy always does.
+template <class S>
+__device__ __forceinline__ const DPrim& prim_at(const S& sc, uint32_t i) { return sc.prims[i]; }
+template <class S, uint32_t I>
+__device__ __forceinline__ DPrim prim_at(const S&, UC<I>) {
+    constexpr DPrim v = S::prims[I];
+    return v;
+}
+template <class S>
+__device__ __forceinline__ const DLight& light_at(const S& sc, uint32_t i) { return sc.lights[i]; }
+template <class S, uint32_t I>
+__device__ __forceinline__ DLight light_at(const S&, UC<I>) {
+    constexpr DLight v = S::lights[I];
+    return v;
+}
+
+template <class S, class F>
+__device__ __forceinline__ void for_each_light(const S& sc, F&& f) {
+    if constexpr (S::kStatic) {
+        static_for<0, S::num_lights>(f);
+    } else {
+#pragma unroll 1
+        for (uint32_t i = 0; i < sc.num_lights; ++i) f(i);
+    }
+}
 
 // ------------------------------------------------------------- SDF program
 __device__ __forceinline__ float len2f(float a, float b) { return __builtin_sqrtf(a * a + b * b); }
@@ -156,55 +214,80 @@ __device__ __forceinline__ f3 sdf_deform(uint32_t op, const uint32_t* __restrict
     return vadd(q, c);
 }
 
-// Evaluate one SDFObject's postfix program at p.  The program counter, the
-// op and the stack pointers are wave-uniform (every lane runs the same
-// program), so the stacks are register arrays indexed by SGPR values.
-__device__ __forceinline__ float sdf_eval(const rrte_sdf_node* __restrict__ nodes, uint32_t count, f3 p) {
-    float vs[RRTE_SDF_MAX_STACK];
-    f3 ps[RRTE_SDF_MAX_POINT_STACK];
-    uint32_t sp = 0, pp = 0;
-    for (uint32_t i = 0; i < count; ++i) {
-        const rrte_sdf_node* __restrict__ n = &nodes[i];
-        uint32_t op = n->op;
-        if (op < 32) {
-            vs[sp] = sdf_leaf(op, n->f, p);
-            ++sp;
-        } else if (op < 64) {
-            float b = vs[sp - 1], a = vs[sp - 2], r;
-            float k = n->f[0];
-            switch (op) {
-            case RRTE_SDF_UNION: r = mn(a, b); break;
-            case RRTE_SDF_DIFFERENCE: r = mx(a, -b); break;
-            case RRTE_SDF_INTERSECTION: r = mx(a, b); break;
-            case RRTE_SDF_SMOOTH_UNION: r = smin(a, b, k); break;
-            case RRTE_SDF_SMOOTH_DIFFERENCE: r = -smin(-a, b, k); break;
-            default: r = -smin(-a, -b, k); break;
-            }
-            sp -= 2;
-            vs[sp] = r;
-            ++sp;
-        } else if (op < 96) {
-            ps[pp] = p;
-            ++pp;
-            p = sdf_deform(op, n->i, n->f, p);
-        } else {
-            --pp;
-            p = ps[pp];
+// One postfix node applied to the value / point stacks (leaves push a
+// distance, CSG ops pop two and push one, deformers push the point and
+// replace it, POP_POINT restores it).
+__device__ __forceinline__ void sdf_node_step(const rrte_sdf_node& n, float* vs, f3* ps, uint32_t& sp, uint32_t& pp,
+                                              f3& p) {
+    const uint32_t op = n.op;
+    if (op < 32) {
+        vs[sp] = sdf_leaf(op, n.f, p);
+        ++sp;
+    } else if (op < 64) {
+        float b = vs[sp - 1], a = vs[sp - 2], r;
+        float k = n.f[0];
+        switch (op) {
+        case RRTE_SDF_UNION: r = mn(a, b); break;
+        case RRTE_SDF_DIFFERENCE: r = mx(a, -b); break;
+        case RRTE_SDF_INTERSECTION: r = mx(a, b); break;
+        case RRTE_SDF_SMOOTH_UNION: r = smin(a, b, k); break;
+        case RRTE_SDF_SMOOTH_DIFFERENCE: r = -smin(-a, b, k); break;
+        default: r = -smin(-a, -b, k); break;
         }
+        sp -= 2;
+        vs[sp] = r;
+        ++sp;
+    } else if (op < 96) {
+        ps[pp] = p;
+        ++pp;
+        p = sdf_deform(op, n.i, n.f, p);
+    } else {
+        --pp;
+        p = ps[pp];
     }
-    return vs[0];
 }
 
-// SDFObject::intersect — sphere tracing inside the object's bounding sphere
-// (build-defined).  March steps and the four tetrahedral
-// normal samples share ONE evaluation site: a lane that has converged keeps
-// evaluating its normal samples while its neighbours are still marching, so
-// the wave never serialises a separate normal pass.  The per-lane trip count
-// diverges; the wave leaves the loop when its EXEC mask drains.
-// NEED_HIT = false (shadow rays) skips the normal samples entirely.
-template <bool NEED_HIT>
-__device__ __forceinline__ bool sdf_intersect(const SceneView& sc, const DPrim& pr, const Ray& r,
-                                              float t_min, float t_max, Hit& out) {
+// Runtime program: the program counter, op and stack pointers are
+// wave-uniform (every lane runs the same program), so the stacks stay in
+// registers indexed by SGPR values.
+struct SdfProgram {
+    const rrte_sdf_node* __restrict__ nodes;
+    uint32_t count;
+    __device__ __forceinline__ float operator()(f3 p) const {
+        float vs[RRTE_SDF_MAX_STACK];
+        f3 ps[RRTE_SDF_MAX_POINT_STACK];
+        uint32_t sp = 0, pp = 0;
+        for (uint32_t i = 0; i < count; ++i) sdf_node_step(nodes[i], vs, ps, sp, pp, p);
+        return vs[0];
+    }
+};
+
+// Static program (scene-specialised kernel): nodes [FIRST, FIRST+COUNT) of a
+// constexpr scene, unrolled at compile time; ops fold, stack slots become
+// fixed registers.
+template <class S, uint32_t FIRST, uint32_t COUNT>
+struct SdfStaticProgram {
+    __device__ __forceinline__ float operator()(f3 p) const {
+        float vs[RRTE_SDF_MAX_STACK];
+        f3 ps[RRTE_SDF_MAX_POINT_STACK];
+        uint32_t sp = 0, pp = 0;
+        auto step = [&](auto jj) {
+            constexpr rrte_sdf_node n = S::nodes[FIRST + decltype(jj)::value];
+            sdf_node_step(n, vs, ps, sp, pp, p);
+        };
+        static_for<0, COUNT>(step);
+        return vs[0];
+    }
+};
+
+// SDFObject::intersect, search part -- sphere tracing inside the object's
+// bounding sphere (build-defined).  Only t is produced here;
+// the closest-hit search keeps (t, object) and the hit attributes are
+// computed once for the winner.  The per-lane trip count diverges; the wave
+// leaves the loop when its EXEC mask drains.
+template <class EVAL>
+__device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
+                                          float& t_hit) {
     f3 bc = V(pr.p[0], pr.p[1], pr.p[2]);
     float br = pr.p[3];
     f3 oc = vsub(r.o, bc);
@@ -216,49 +299,40 @@ __device__ __forceinline__ bool sdf_intersect(const SceneView& sc, const DPrim& 
     float t = mx(t_min, -b - sq);
     float tend = mn(t_max, -b + sq);
     if (t > tend) return false;
-    const rrte_sdf_node* __restrict__ nodes = sc.nodes + pr.sdf_first;
-    const uint32_t count = pr.sdf_count;
     const float eps = pr.sdf_hit_eps, scale = pr.sdf_step_scale;
     const uint32_t steps = pr.sdf_max_steps;
-    if (steps == 0) return false;
-    const float h = 1e-3f;
-    f3 p = V(0.0f, 0.0f, 0.0f), n = V(0.0f, 0.0f, 0.0f);
-    uint32_t i = 0, phase = 0;  // phase 0: marching; 1..4: normal sample phase-1
-    bool result = false;
-    for (;;) {
-        f3 q;
-        if (phase == 0) {
-            q = ray_at(r, t);
-        } else {
-            // tetrahedron offsets k0=(+,-,-) k1=(-,-,+) k2=(-,+,-) k3=(+,+,+)
-            bool sx = (phase == 1) || (phase == 4);
-            bool sy = (phase >= 3);
-            bool sz = (phase == 2) || (phase == 4);
-            q = V(sx ? p.x + h : p.x - h, sy ? p.y + h : p.y - h, sz ? p.z + h : p.z - h);
+#pragma unroll 1
+    for (uint32_t i = 0; i < steps; ++i) {
+        f3 p = ray_at(r, t);
+        float d = eval(p);
+        if (d < eps * t) {
+            t_hit = t;
+            return true;
         }
-        float d = sdf_eval(nodes, count, q);
-        if (phase == 0) {
-            if (d < eps * t) {
-                if (!NEED_HIT) { result = true; break; }
-                p = q;
-                phase = 1;
-                continue;
-            }
-            t = t + d * scale;
-            ++i;
-            if (t > tend || i >= steps) break;
-        } else {
-            // n = k0 f0 + k1 f1 + k2 f2 + k3 f3, accumulated in the oracle's order
-            if (phase == 1) { n.x = d; n.y = -d; n.z = -d; }
-            else if (phase == 2) { n.x = n.x - d; n.y = n.y - d; n.z = n.z + d; }
-            else if (phase == 3) { n.x = n.x - d; n.y = n.y + d; n.z = n.z - d; }
-            else { n.x = n.x + d; n.y = n.y + d; n.z = n.z + d; }
-            ++phase;
-            if (phase == 5) { result = true; break; }
-        }
+        t = t + d * scale;
+        if (t > tend) return false;
     }
-    if (NEED_HIT && result) hit_new(out, t, p, vnorm(n), r);
-    return result;
+    return false;
+}
+
+// Hit attributes of an SDF hit at t: p = Ray::at(t) and the tetrahedral
+// normal n = sum_k k_i f(p + k_i h), h = 1e-3, accumulated in the oracle's
+// order: k0=(+,-,-) k1=(-,-,+) k2=(-,+,-) k3=(+,+,+).  One evaluation site.
+template <class EVAL>
+__device__ __forceinline__ void sdf_hit_attributes(const EVAL& eval, const Ray& r, float t, Hit& out) {
+    const float h = 1e-3f;
+    f3 p = ray_at(r, t), n = V(0.0f, 0.0f, 0.0f);
+#pragma unroll 1
+    for (uint32_t k = 0; k < 4; ++k) {
+        bool sx = (k == 0) || (k == 3), sy = (k >= 2), sz = (k == 1) || (k == 3);
+        f3 q = V(sx ? p.x + h : p.x - h, sy ? p.y + h : p.y - h, sz ? p.z + h : p.z - h);
+        float d = eval(q);
+        if (k == 0) { n.x = d; n.y = -d; n.z = -d; }
+        else if (k == 1) { n.x = n.x - d; n.y = n.y - d; n.z = n.z + d; }
+        else if (k == 2) { n.x = n.x - d; n.y = n.y + d; n.z = n.z - d; }
+        else { n.x = n.x + d; n.y = n.y + d; n.z = n.z + d; }
+    }
+    hit_new(out, t, p, vnorm(n), r);
 }
 
 // ----------------------------------------------------- analytic intersectors
@@ -267,202 +341,190 @@ __device__ __forceinline__ void local_ray(const DPrim& pr, const Ray& r, Ray& lr
     lr = ray_new(m_point(pr.inv, r.o), vnorm(m_vector(pr.inv, r.d)));
 }
 
-// SceneObject::intersect (primitives.rs:57-725)
+// ----------------------------------------------------- analytic intersectors
+// SceneObject::intersect for the seven primitive kinds (primitives.rs:57-725).
+// t is always written to out.t; point/normal only matter when NEED_HIT.
 template <bool NEED_HIT>
-__device__ __forceinline__ bool intersect(const SceneView& sc, const DPrim& pr, const Ray& r,
-                                          float t_min, float t_max, Hit& out) {
-    switch (pr.kind) {
-    case RRTE_PRIM_SPHERE: {  // primitives.rs:57-81
-        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
-        float rad = pr.p[3];
-        f3 oc = vsub(r.o, ctr);
-        float a = vlen2(r.d);
-        float hb = vdot(oc, r.d);
+__device__ __forceinline__ bool isect_sphere(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:57-81
+    f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+    float rad = pr.p[3];
+    f3 oc = vsub(r.o, ctr);
+    float a = vlen2(r.d);
+    float hb = vdot(oc, r.d);
+    float cc = vlen2(oc) - rad * rad;
+    float disc = hb * hb - a * cc;
+    if (disc < 0.0f) return false;
+    float sq = __builtin_sqrtf(disc);
+    float root = (-hb - sq) / a;
+    if (root < t_min || t_max < root) {
+        root = (-hb + sq) / a;
+        if (root < t_min || t_max < root) return false;
+    }
+    f3 p = ray_at(r, root);
+    hit_new(out, root, p, vdivs(vsub(p, ctr), rad), r);
+    return true;
+}
+
+template <bool NEED_HIT>
+__device__ __forceinline__ bool isect_plane(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:133-149
+    f3 pt = V(pr.p[0], pr.p[1], pr.p[2]), n = V(pr.p[4], pr.p[5], pr.p[6]);
+    float denom = vdot(n, r.d);
+    if (fabsf(denom) < 1e-6f) return false;
+    float t = vdot(vsub(pt, r.o), n) / denom;
+    if (t < t_min || t > t_max) return false;
+    f3 p = ray_at(r, t);
+    hit_new(out, t, p, denom < 0.0f ? n : vneg(n), r);
+    return true;
+}
+
+template <bool NEED_HIT>
+__device__ __forceinline__ bool isect_triangle(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:208-244
+    f3 v0 = V(pr.p[0], pr.p[1], pr.p[2]), v1 = V(pr.p[3], pr.p[4], pr.p[5]), v2 = V(pr.p[6], pr.p[7], pr.p[8]);
+    f3 e1 = vsub(v1, v0), e2 = vsub(v2, v0);
+    f3 h = vcross(r.d, e2);
+    float a = vdot(e1, h);
+    if (a > -1e-6f && a < 1e-6f) return false;
+    float f = 1.0f / a;
+    f3 s = vsub(r.o, v0);
+    float u = f * vdot(s, h);
+    if (u < 0.0f || u > 1.0f) return false;
+    f3 q = vcross(s, e1);
+    float v = f * vdot(r.d, q);
+    if (v < 0.0f || u + v > 1.0f) return false;
+    float t = f * vdot(e2, q);
+    if (t < t_min || t > t_max) return false;
+    f3 p = ray_at(r, t);
+    float w = 1.0f - u - v;
+    f3 n0 = V(pr.p[9], pr.p[10], pr.p[11]), n1 = V(pr.p[12], pr.p[13], pr.p[14]),
+       n2 = V(pr.p[15], pr.p[16], pr.p[17]);
+    f3 n = vnorm(vadd(vadd(vmuls(n0, w), vmuls(n1, u)), vmuls(n2, v)));
+    hit_new(out, t, p, n, r);
+    return true;
+}
+
+template <bool NEED_HIT>
+__device__ __forceinline__ bool isect_cube(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:301-364
+    Ray lr;
+    local_ray(pr, r, lr);
+    f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]), size = V(pr.p[4], pr.p[5], pr.p[6]);
+    f3 half = vmuls(size, 0.5f);
+    f3 mnb = vsub(ctr, half), mxb = vadd(ctr, half);
+    float t_near = t_min, t_far = t_max;
+    f3 normal = V(0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (uint32_t i = 0; i < 3; ++i) {
+        f3 axis = setcomp(V(0.0f, 0.0f, 0.0f), i, 1.0f);
+        float oc = vdot(lr.o, axis), dc = vdot(lr.d, axis);
+        float lo = vdot(mnb, axis), hi = vdot(mxb, axis);
+        if (fabsf(dc) < 1e-6f) {
+            if (oc < lo || oc > hi) return false;
+        } else {
+            float t1 = (lo - oc) / dc, t2 = (hi - oc) / dc;
+            float tsn = t1 < t2 ? t1 : t2, tsf = t1 < t2 ? t2 : t1;
+            if (tsn > t_near) {
+                t_near = tsn;
+                normal = t1 < t2 ? vneg(axis) : axis;
+            }
+            if (tsf < t_far) t_far = tsf;
+            if (t_near > t_far) return false;
+        }
+    }
+    float t = (t_near >= t_min) ? t_near : t_far;
+    if (t < t_min || t > t_max) return false;
+    f3 lp = ray_at(lr, t);
+    hit_new(out, t, m_point(pr.xf, lp), vnorm(m_vector(pr.xf, normal)), r);
+    return true;
+}
+
+template <bool NEED_HIT>
+__device__ __forceinline__ bool isect_cylinder(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:419-465
+    Ray lr;
+    local_ray(pr, r, lr);
+    f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+    float rad = pr.p[3], hh = pr.p[4] * 0.5f;
+    f3 oc = vsub(lr.o, ctr);
+    float a = lr.d.x * lr.d.x + lr.d.z * lr.d.z;
+    float b = 2.0f * (oc.x * lr.d.x + oc.z * lr.d.z);
+    float cc = oc.x * oc.x + oc.z * oc.z - rad * rad;
+    float disc = b * b - 4.0f * a * cc;
+    if (disc < 0.0f) return false;
+    float sq = __builtin_sqrtf(disc);
+    float ts0 = (-b - sq) / (2.0f * a), ts1 = (-b + sq) / (2.0f * a);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        float t = k == 0 ? ts0 : ts1;
+        if (t >= t_min && t <= t_max) {
+            f3 p = ray_at(lr, t);
+            if (fabsf(p.y - ctr.y) <= hh) {
+                f3 ln = V((p.x - ctr.x) / rad, 0.0f, (p.z - ctr.z) / rad);
+                hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
+template <bool NEED_HIT>
+__device__ __forceinline__ bool isect_cone(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:520-571
+    Ray lr;
+    local_ray(pr, r, lr);
+    f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+    float rad = pr.p[3], ht = pr.p[4], hh = ht * 0.5f;
+    f3 oc = vsub(lr.o, ctr);
+    float k = rad / ht, k2 = k * k;
+    f3 d = lr.d;
+    float a = d.x * d.x + d.z * d.z - k2 * d.y * d.y;
+    float b = 2.0f * (oc.x * d.x + oc.z * d.z - k2 * (oc.y - hh) * d.y);
+    float cc = oc.x * oc.x + oc.z * oc.z - k2 * (oc.y - hh) * (oc.y - hh);
+    float disc = b * b - 4.0f * a * cc;
+    if (disc < 0.0f) return false;
+    float sq = __builtin_sqrtf(disc);
+    float ts0 = (-b - sq) / (2.0f * a), ts1 = (-b + sq) / (2.0f * a);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        float t = kk == 0 ? ts0 : ts1;
+        if (t >= t_min && t <= t_max) {
+            f3 p = ray_at(lr, t);
+            float yl = p.y - ctr.y;
+            if (yl >= -hh && yl <= hh) {
+                float rr = __builtin_sqrtf(p.x * p.x + p.z * p.z);
+                f3 ln = vnorm(V(p.x / rr, k, p.z / rr));
+                hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
+template <bool NEED_HIT>
+__device__ __forceinline__ bool isect_capsule(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:626-725
+    Ray lr;
+    local_ray(pr, r, lr);
+    f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+    float rad = pr.p[3], hh = pr.p[4] * 0.5f;
+    float closest = kInf;
+    bool found = false;
+    float a = vlen2(lr.d);
+#pragma unroll
+    for (int cap = 0; cap < 2; ++cap) {
+        f3 cc_ = cap == 0 ? vadd(ctr, V(0.0f, hh, 0.0f)) : vsub(ctr, V(0.0f, hh, 0.0f));
+        f3 oc = vsub(lr.o, cc_);
+        float hb = vdot(oc, lr.d);
         float cc = vlen2(oc) - rad * rad;
         float disc = hb * hb - a * cc;
-        if (disc < 0.0f) return false;
-        float sq = __builtin_sqrtf(disc);
-        float root = (-hb - sq) / a;
-        if (root < t_min || t_max < root) {
-            root = (-hb + sq) / a;
-            if (root < t_min || t_max < root) return false;
-        }
-        f3 p = ray_at(r, root);
-        hit_new(out, root, p, vdivs(vsub(p, ctr), rad), r);
-        return true;
-    }
-    case RRTE_PRIM_PLANE: {  // primitives.rs:133-149
-        f3 pt = V(pr.p[0], pr.p[1], pr.p[2]), n = V(pr.p[4], pr.p[5], pr.p[6]);
-        float denom = vdot(n, r.d);
-        if (fabsf(denom) < 1e-6f) return false;
-        float t = vdot(vsub(pt, r.o), n) / denom;
-        if (t < t_min || t > t_max) return false;
-        f3 p = ray_at(r, t);
-        hit_new(out, t, p, denom < 0.0f ? n : vneg(n), r);
-        return true;
-    }
-    case RRTE_PRIM_TRIANGLE: {  // primitives.rs:208-244
-        f3 v0 = V(pr.p[0], pr.p[1], pr.p[2]), v1 = V(pr.p[3], pr.p[4], pr.p[5]), v2 = V(pr.p[6], pr.p[7], pr.p[8]);
-        f3 e1 = vsub(v1, v0), e2 = vsub(v2, v0);
-        f3 h = vcross(r.d, e2);
-        float a = vdot(e1, h);
-        if (a > -1e-6f && a < 1e-6f) return false;
-        float f = 1.0f / a;
-        f3 s = vsub(r.o, v0);
-        float u = f * vdot(s, h);
-        if (u < 0.0f || u > 1.0f) return false;
-        f3 q = vcross(s, e1);
-        float v = f * vdot(r.d, q);
-        if (v < 0.0f || u + v > 1.0f) return false;
-        float t = f * vdot(e2, q);
-        if (t < t_min || t > t_max) return false;
-        f3 p = ray_at(r, t);
-        float w = 1.0f - u - v;
-        f3 n0 = V(pr.p[9], pr.p[10], pr.p[11]), n1 = V(pr.p[12], pr.p[13], pr.p[14]),
-           n2 = V(pr.p[15], pr.p[16], pr.p[17]);
-        f3 n = vnorm(vadd(vadd(vmuls(n0, w), vmuls(n1, u)), vmuls(n2, v)));
-        hit_new(out, t, p, n, r);
-        return true;
-    }
-    case RRTE_PRIM_CUBE: {  // primitives.rs:301-364
-        Ray lr;
-        local_ray(pr, r, lr);
-        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]), size = V(pr.p[4], pr.p[5], pr.p[6]);
-        f3 half = vmuls(size, 0.5f);
-        f3 mnb = vsub(ctr, half), mxb = vadd(ctr, half);
-        float t_near = t_min, t_far = t_max;
-        f3 normal = V(0.0f, 0.0f, 0.0f);
-#pragma unroll
-        for (uint32_t i = 0; i < 3; ++i) {
-            f3 axis = setcomp(V(0.0f, 0.0f, 0.0f), i, 1.0f);
-            float oc = vdot(lr.o, axis), dc = vdot(lr.d, axis);
-            float lo = vdot(mnb, axis), hi = vdot(mxb, axis);
-            if (fabsf(dc) < 1e-6f) {
-                if (oc < lo || oc > hi) return false;
-            } else {
-                float t1 = (lo - oc) / dc, t2 = (hi - oc) / dc;
-                float tsn = t1 < t2 ? t1 : t2, tsf = t1 < t2 ? t2 : t1;
-                if (tsn > t_near) {
-                    t_near = tsn;
-                    normal = t1 < t2 ? vneg(axis) : axis;
-                }
-                if (tsf < t_far) t_far = tsf;
-                if (t_near > t_far) return false;
-            }
-        }
-        float t = (t_near >= t_min) ? t_near : t_far;
-        if (t < t_min || t > t_max) return false;
-        f3 lp = ray_at(lr, t);
-        hit_new(out, t, m_point(pr.xf, lp), vnorm(m_vector(pr.xf, normal)), r);
-        return true;
-    }
-    case RRTE_PRIM_CYLINDER: {  // primitives.rs:419-465
-        Ray lr;
-        local_ray(pr, r, lr);
-        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
-        float rad = pr.p[3], hh = pr.p[4] * 0.5f;
-        f3 oc = vsub(lr.o, ctr);
-        float a = lr.d.x * lr.d.x + lr.d.z * lr.d.z;
-        float b = 2.0f * (oc.x * lr.d.x + oc.z * lr.d.z);
-        float cc = oc.x * oc.x + oc.z * oc.z - rad * rad;
-        float disc = b * b - 4.0f * a * cc;
-        if (disc < 0.0f) return false;
-        float sq = __builtin_sqrtf(disc);
-        float ts0 = (-b - sq) / (2.0f * a), ts1 = (-b + sq) / (2.0f * a);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            float t = k == 0 ? ts0 : ts1;
-            if (t >= t_min && t <= t_max) {
-                f3 p = ray_at(lr, t);
-                if (fabsf(p.y - ctr.y) <= hh) {
-                    f3 ln = V((p.x - ctr.x) / rad, 0.0f, (p.z - ctr.z) / rad);
-                    hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
-                    return true;
-                }
-            }
-        }
-        return false;
-    }
-    case RRTE_PRIM_CONE: {  // primitives.rs:520-571
-        Ray lr;
-        local_ray(pr, r, lr);
-        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
-        float rad = pr.p[3], ht = pr.p[4], hh = ht * 0.5f;
-        f3 oc = vsub(lr.o, ctr);
-        float k = rad / ht, k2 = k * k;
-        f3 d = lr.d;
-        float a = d.x * d.x + d.z * d.z - k2 * d.y * d.y;
-        float b = 2.0f * (oc.x * d.x + oc.z * d.z - k2 * (oc.y - hh) * d.y);
-        float cc = oc.x * oc.x + oc.z * oc.z - k2 * (oc.y - hh) * (oc.y - hh);
-        float disc = b * b - 4.0f * a * cc;
-        if (disc < 0.0f) return false;
-        float sq = __builtin_sqrtf(disc);
-        float ts0 = (-b - sq) / (2.0f * a), ts1 = (-b + sq) / (2.0f * a);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            float t = kk == 0 ? ts0 : ts1;
-            if (t >= t_min && t <= t_max) {
-                f3 p = ray_at(lr, t);
-                float yl = p.y - ctr.y;
-                if (yl >= -hh && yl <= hh) {
-                    float rr = __builtin_sqrtf(p.x * p.x + p.z * p.z);
-                    f3 ln = vnorm(V(p.x / rr, k, p.z / rr));
-                    hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
-                    return true;
-                }
-            }
-        }
-        return false;
-    }
-    case RRTE_PRIM_CAPSULE: {  // primitives.rs:626-725
-        Ray lr;
-        local_ray(pr, r, lr);
-        f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
-        float rad = pr.p[3], hh = pr.p[4] * 0.5f;
-        float closest = kInf;
-        bool found = false;
-        float a = vlen2(lr.d);
-#pragma unroll
-        for (int cap = 0; cap < 2; ++cap) {
-            f3 cc_ = cap == 0 ? vadd(ctr, V(0.0f, hh, 0.0f)) : vsub(ctr, V(0.0f, hh, 0.0f));
-            f3 oc = vsub(lr.o, cc_);
-            float hb = vdot(oc, lr.d);
-            float cc = vlen2(oc) - rad * rad;
-            float disc = hb * hb - a * cc;
-            if (disc >= 0.0f) {
-                float sq = __builtin_sqrtf(disc);
-                float ts0 = (-hb - sq) / a, ts1 = (-hb + sq) / a;
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    float t = k == 0 ? ts0 : ts1;
-                    if (t >= t_min && t <= t_max && t < closest) {
-                        f3 p = ray_at(lr, t);
-                        bool ok = cap == 0 ? (p.y >= ctr.y) : (p.y <= ctr.y);
-                        if (ok) {
-                            f3 ln = vnorm(vsub(p, cc_));
-                            closest = t;
-                            hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
-                            found = true;
-                        }
-                    }
-                }
-            }
-        }
-        f3 oc = vsub(lr.o, ctr);
-        float ac = lr.d.x * lr.d.x + lr.d.z * lr.d.z;
-        float bc = 2.0f * (oc.x * lr.d.x + oc.z * lr.d.z);
-        float ccy = oc.x * oc.x + oc.z * oc.z - rad * rad;
-        float disc = bc * bc - 4.0f * ac * ccy;
         if (disc >= 0.0f) {
             float sq = __builtin_sqrtf(disc);
-            float ts0 = (-bc - sq) / (2.0f * ac), ts1 = (-bc + sq) / (2.0f * ac);
+            float ts0 = (-hb - sq) / a, ts1 = (-hb + sq) / a;
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 float t = k == 0 ? ts0 : ts1;
                 if (t >= t_min && t <= t_max && t < closest) {
                     f3 p = ray_at(lr, t);
-                    if (fabsf(p.y - ctr.y) <= hh) {
-                        f3 ln = V((p.x - ctr.x) / rad, 0.0f, (p.z - ctr.z) / rad);
+                    bool ok = cap == 0 ? (p.y >= ctr.y) : (p.y <= ctr.y);
+                    if (ok) {
+                        f3 ln = vnorm(vsub(p, cc_));
                         closest = t;
                         hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
                         found = true;
@@ -470,42 +532,163 @@ __device__ __forceinline__ bool intersect(const SceneView& sc, const DPrim& pr, 
                 }
             }
         }
-        return found;
     }
+    f3 oc = vsub(lr.o, ctr);
+    float ac = lr.d.x * lr.d.x + lr.d.z * lr.d.z;
+    float bc = 2.0f * (oc.x * lr.d.x + oc.z * lr.d.z);
+    float ccy = oc.x * oc.x + oc.z * oc.z - rad * rad;
+    float disc = bc * bc - 4.0f * ac * ccy;
+    if (disc >= 0.0f) {
+        float sq = __builtin_sqrtf(disc);
+        float ts0 = (-bc - sq) / (2.0f * ac), ts1 = (-bc + sq) / (2.0f * ac);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            float t = k == 0 ? ts0 : ts1;
+            if (t >= t_min && t <= t_max && t < closest) {
+                f3 p = ray_at(lr, t);
+                if (fabsf(p.y - ctr.y) <= hh) {
+                    f3 ln = V((p.x - ctr.x) / rad, 0.0f, (p.z - ctr.z) / rad);
+                    closest = t;
+                    hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
+                    found = true;
+                }
+            }
+        }
+    }
+    return found;
+}
+
+template <bool NEED_HIT, class EVAL>
+__device__ __forceinline__ bool isect_sdf(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
+                                          Hit& out) {
+    float t;
+    if (!sdf_march(pr, eval, r, t_min, t_max, t)) return false;
+    if (NEED_HIT) sdf_hit_attributes(eval, r, t, out);
+    else out.t = t;
+    return true;
+}
+
+// SceneObject::intersect dispatch, runtime object index: switch on the kind
+// (wave-uniform -> scalar branches).
+template <bool NEED_HIT, class S>
+__device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t_max,
+                                             Hit& out) {
+    const DPrim& pr = sc.prims[i];
+    switch (pr.kind) {
+    case RRTE_PRIM_SPHERE: return isect_sphere<NEED_HIT>(pr, r, t_min, t_max, out);
+    case RRTE_PRIM_PLANE: return isect_plane<NEED_HIT>(pr, r, t_min, t_max, out);
+    case RRTE_PRIM_TRIANGLE: return isect_triangle<NEED_HIT>(pr, r, t_min, t_max, out);
+    case RRTE_PRIM_CUBE: return isect_cube<NEED_HIT>(pr, r, t_min, t_max, out);
+    case RRTE_PRIM_CYLINDER: return isect_cylinder<NEED_HIT>(pr, r, t_min, t_max, out);
+    case RRTE_PRIM_CONE: return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
+    case RRTE_PRIM_CAPSULE: return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
     case RRTE_PRIM_SDF:
-        return sdf_intersect<NEED_HIT>(sc, pr, r, t_min, t_max, out);
-    default:
-        return false;
+        return isect_sdf<NEED_HIT>(pr, SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t_min, t_max, out);
+    default: return false;
     }
+}
+
+// Compile-time object index (scene-specialised kernel): only the object's
+// own intersector is instantiated.
+template <bool NEED_HIT, class S, uint32_t I>
+__device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, float t_min, float t_max, Hit& out) {
+    constexpr DPrim pr = S::prims[I];
+    constexpr uint32_t kind = pr.kind;
+    if constexpr (kind == RRTE_PRIM_SPHERE) return isect_sphere<NEED_HIT>(pr, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_PLANE) return isect_plane<NEED_HIT>(pr, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_TRIANGLE) return isect_triangle<NEED_HIT>(pr, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_CUBE) return isect_cube<NEED_HIT>(pr, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_CYLINDER) return isect_cylinder<NEED_HIT>(pr, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_CONE) return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_CAPSULE) return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_SDF)
+        return isect_sdf<NEED_HIT>(pr, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t_min, t_max, out);
+    else return false;
 }
 
 // Closest hit over all objects (raytracer.rs:103-113): strict '<' keeps the
 // earlier object on ties; analytic objects get t_max = INFINITY as in the
-// reference, SDF objects march only up to the current closest hit.
-__device__ __forceinline__ int closest_hit(const SceneView& sc, const Ray& r, float t_min, Hit& best) {
+// reference, SDF objects march only up to the current closest hit.  The
+// search carries only (t, object); attributes are produced afterwards.
+template <class S>
+__device__ __forceinline__ int closest_t(const S& sc, const Ray& r, float t_min, float& best_t) {
     int idx = -1;
-    for (uint32_t i = 0; i < sc.num_prims; ++i) {
-        const DPrim& pr = sc.prims[i];
+    best_t = kInf;
+    for_each_prim(sc, [&](auto ii) {
+        const uint32_t i = ii;
         Hit h;
-        float tmax = (pr.kind == RRTE_PRIM_SDF && idx >= 0) ? best.t : kInf;
-        if (intersect<true>(sc, pr, r, t_min, tmax, h)) {
-            if (idx < 0 || h.t < best.t) {
-                best = h;
+        float tmax = (prim_at(sc, ii).kind == RRTE_PRIM_SDF && idx >= 0) ? best_t : kInf;
+        if (intersect_at<false>(sc, ii, r, t_min, tmax, h)) {
+            if (idx < 0 || h.t < best_t) {
+                best_t = h.t;
                 idx = (int)i;
             }
         }
+    });
+    return idx;
+}
+
+// Hit attributes for the winning object of each lane: analytic objects are
+// re-intersected with the search's exact arguments, SDF objects evaluate
+// point + normal at the found t -- bit-identical to computing them during the
+// search.  Runtime scene: the wave walks its distinct winners (readfirstlane
+// -> uniform object index -> scalar loads).  Static scene: every object is
+// visited with a compile-time index and skipped unless some lane won it.
+template <class S>
+__device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t, Hit& out) {
+    const DPrim& pr = sc.prims[i];
+    if (pr.kind == RRTE_PRIM_SDF) sdf_hit_attributes(SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t, out);
+    else intersect_at<true>(sc, i, r, t_min, kInf, out);
+}
+template <class S, uint32_t I>
+__device__ __forceinline__ void attributes_at(const S& sc, UC<I> ii, const Ray& r, float t_min, float t, Hit& out) {
+    constexpr DPrim pr = S::prims[I];
+    if constexpr (pr.kind == RRTE_PRIM_SDF)
+        sdf_hit_attributes(SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t, out);
+    else
+        intersect_at<true>(sc, ii, r, t_min, kInf, out);
+}
+
+template <class S>
+__device__ __forceinline__ void hit_attributes(const S& sc, const Ray& r, float t_min, int idx, float t,
+                                               Hit& out) {
+    if constexpr (S::kStatic) {
+        for_each_prim(sc, [&](auto ii) {
+            const uint32_t i = ii;
+            if (__any((uint32_t)idx == i)) {
+                if ((uint32_t)idx == i) attributes_at(sc, ii, r, t_min, t, out);
+            }
+        });
+    } else {
+        bool pending = idx >= 0;
+        while (pending) {
+            const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)idx);
+            if ((uint32_t)idx == i) {
+                attributes_at(sc, i, r, t_min, t, out);
+                pending = false;
+            }
+        }
     }
+}
+
+template <class S>
+__device__ __forceinline__ int closest_hit(const S& sc, const Ray& r, float t_min, Hit& best) {
+    float t;
+    int idx = closest_t(sc, r, t_min, t);
+    hit_attributes(sc, r, t_min, idx, t, best);
     return idx;
 }
 
 // Any hit in [t_min, t_max] (LAMBERT_SHADOW shadow rays).
-__device__ __forceinline__ bool occluded(const SceneView& sc, const Ray& r, float t_min, float t_max) {
-    bool hit_any = false;
-    for (uint32_t i = 0; i < sc.num_prims; ++i) {
+template <class S>
+__device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min, float t_max) {
+    bool hit_any = false, all_done = false;
+    for_each_prim(sc, [&](auto ii) {
+        if (all_done) return;  // wave-uniform: every active lane already occluded
         Hit h;
-        if (!hit_any && intersect<false>(sc, sc.prims[i], r, t_min, t_max, h)) hit_any = true;
-        if (__all(hit_any)) break;  // every active lane already occluded
-    }
+        if (!hit_any && intersect_at<false>(sc, ii, r, t_min, t_max, h)) hit_any = true;
+        all_done = __all(hit_any);
+    });
     return hit_any;
 }
 
@@ -644,13 +827,17 @@ __device__ __forceinline__ Ray generate_ray(const KParams& kp, float u, float v)
 // evaluated forward with a running albedo product; that is bit-identical to
 // the recursion for max_depth <= 2 (the parity configs use 1) and differs by
 // rounding only beyond.
-template <int MODE>
-__device__ __forceinline__ Col ray_color(const SceneView& sc, const KParams& kp, Ray r, uint32_t& st,
+// SINGLE (scene-specialised kernels): exactly one bounce -- the host only
+// selects it when max_depth == 1 or the mode is LAMBERT_SHADOW -- so the
+// kernel is straight-line code apart from the march loops.
+template <int MODE, class S, bool SINGLE>
+__device__ __forceinline__ Col ray_color(const S& sc, const KParams& kp, Ray r, uint32_t& st,
                                          uint32_t& nshadow) {
     Col out{0.0f, 0.0f, 0.0f, 1.0f};
     if (kp.max_depth == 0) return out;
     float tr = 1.0f, tg = 1.0f, tb = 1.0f;  // running albedo product
-    for (uint32_t depth = 0; depth < kp.max_depth; ++depth) {
+    const uint32_t ndepth = SINGLE ? 1u : kp.max_depth;
+    for (uint32_t depth = 0; depth < ndepth; ++depth) {
         Hit h;
         int idx = closest_hit(sc, r, kp.t_min, h);
         if (idx < 0) {
@@ -661,6 +848,10 @@ __device__ __forceinline__ Col ray_color(const SceneView& sc, const KParams& kp,
                 out.g = out.g + tg * kp.bg[1];
                 out.b = out.b + tb * kp.bg[2];
             }
+            break;
+        }
+        if (kp.debug & 2u) {  // primary visibility only
+            out = Col{h.t * 0.01f, 0.0f, 0.0f, 1.0f};
             break;
         }
         const DPrim& pr = sc.prims[idx];
@@ -674,36 +865,36 @@ __device__ __forceinline__ Col ray_color(const SceneView& sc, const KParams& kp,
         float cb = 0.0f + (ab * 0.1f) * 0.1f;
         float ca = 1.0f + (aa * 0.1f) * 0.1f;
         if (MODE == RRTE_MODE_REFCOMPAT) {
-            for (uint32_t li = 0; li < sc.num_lights; ++li) {
-                Contrib k = illuminate(sc.lights[li], h.p);
+            for_each_light(sc, [&](auto lii) {
+                Contrib k = illuminate(light_at(sc, lii), h.p);
                 cr = cr + k.cr * k.att;
                 cg = cg + k.cg * k.att;
                 cb = cb + k.cb * k.att;
                 ca = ca + k.ca * k.att;
-            }
+            });
         } else {
             const float bias = kp.bias;
-            for (uint32_t li = 0; li < sc.num_lights; ++li) {
-                const DLight& l = sc.lights[li];
+            for_each_light(sc, [&](auto lii) {
+                const auto& l = light_at(sc, lii);
                 Contrib k = illuminate(l, h.p);
                 if (l.kind == RRTE_LIGHT_AMBIENT) {
                     cr = cr + ar * k.cr;
                     cg = cg + ag * k.cg;
                     cb = cb + ab * k.cb;
-                    continue;
+                    return;
                 }
                 float ndl = vdot(h.n, k.dir);
                 if (ndl > 0.0f && k.att > 0.0f) {
                     ++nshadow;
                     Ray sr = ray_new(vadd(h.p, vmuls(h.n, bias)), k.dir);
-                    if (!occluded(sc, sr, bias, k.dist)) {
+                    if ((kp.debug & 1u) || !occluded(sc, sr, bias, k.dist)) {
                         float f = k.att * ndl;
                         cr = cr + ar * (k.cr * f);
                         cg = cg + ag * (k.cg * f);
                         cb = cb + ab * (k.cb * f);
                     }
                 }
-            }
+            });
         }
         if (depth == 0) {
             out = Col{cr, cg, cb, ca};
@@ -746,10 +937,10 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
 }
 
 // One lane per pixel; wave = 8x8 tile, workgroup = 16x16 pixels.
-template <int MODE>
-__global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, uint32_t* __restrict__ out_rgba8,
-                                                  float4* __restrict__ out_f32,
-                                                  unsigned long long* __restrict__ counters) {
+template <int MODE, class S, bool SINGLE = false>
+__device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, uint32_t* __restrict__ out_rgba8,
+                                                float4* __restrict__ out_f32,
+                                                unsigned long long* __restrict__ counters) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t lr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
@@ -758,7 +949,8 @@ __global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, uint
         const uint32_t y = image_row(kp, lr);
         const uint32_t pix = y * kp.width + x;
         Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
-        for (uint32_t s = 0; s < kp.spp; ++s) {
+        const uint32_t nsamples = SINGLE ? 1u : kp.spp;
+        for (uint32_t s = 0; s < nsamples; ++s) {
             uint32_t st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
             float jx = 0.5f, jy = 0.5f;
             if (kp.jitter == RRTE_JITTER_RANDOM) {
@@ -768,7 +960,7 @@ __global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, uint
             float u = ((float)x + jx) / (float)kp.width;
             float v = ((float)y + jy) / (float)kp.height;
             Ray r = generate_ray(kp, u, v);
-            Col c = ray_color<MODE>(sc, kp, r, st, nshadow);
+            Col c = ray_color<MODE, S, SINGLE>(sc, kp, r, st, nshadow);
             acc.r = acc.r + c.r;
             acc.g = acc.g + c.g;
             acc.b = acc.b + c.b;
@@ -798,6 +990,14 @@ __global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, uint
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
         if (lane == 0 && v) atomicAdd(counters, (unsigned long long)v);
     }
+}
+
+// Generic kernel: the scene is read from HBM through wave-uniform (scalar) loads.
+template <int MODE>
+__global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, uint32_t* __restrict__ out_rgba8,
+                                                  float4* __restrict__ out_f32,
+                                                  unsigned long long* __restrict__ counters) {
+    ray_kernel_body<MODE, SceneView>(kp, sc, out_rgba8, out_f32, counters);
 }
 
 // Root-side de-interleave after the RCCL gather: the gathered buffer holds

@@ -11,13 +11,16 @@
 #include <rccl/rccl.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
+#include "jit.hpp"
 #include "ray_kernels.hpp"
 
 using namespace rrte;
@@ -49,6 +52,15 @@ struct rrte_ctx {
     rrte_stats stats{};
     bool pending_kernel_timing = false;
     uint64_t pending_primary = 0;
+    // scene-specialised kernels (jit.hip)
+    int jit_mode = RRTE_JIT_AUTO;
+    uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
+    std::vector<DPrim> h_prims;                  // host copy of the lowered scene (JIT source)
+    std::vector<DMaterial> h_mats;
+    std::vector<DLight> h_lights;
+    std::vector<rrte_sdf_node> h_nodes;
+    std::unordered_map<std::string, JitKernel> jit_cache;  // failed compiles cached with fn == nullptr
+    std::string jit_log;
 };
 
 namespace {
@@ -205,23 +217,11 @@ rrte_status validate(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_para
     return RRTE_OK;
 }
 
-// Upload the scene if it differs from the cached copy (the analogue of
-// caching on Scene::is_dirty, crates/rrte-scene/src/lib.rs:310-312).
-rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
-    const size_t bp = sizeof(rrte_prim) * s->num_prims, bm = sizeof(rrte_material) * s->num_materials,
-                 bl = sizeof(rrte_light) * s->num_lights, bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
-    const size_t key_len = bp + bm + bl + bn + 4 * sizeof(uint32_t);
-    bool same = c->scene_key.size() == key_len;
-    if (same) {
-        const unsigned char* k = c->scene_key.data();
-        same = (bp == 0 || !memcmp(k, s->prims, bp)) && (bm == 0 || !memcmp(k + bp, s->materials, bm)) &&
-               (bl == 0 || !memcmp(k + bp + bm, s->lights, bl)) &&
-               (bn == 0 || !memcmp(k + bp + bm + bl, s->sdf_nodes, bn));
-    }
-    *upload_ms = 0.0;
-    if (same) return RRTE_OK;
-
-    std::vector<DPrim> prims(s->num_prims);
+// Lower the ABI records to device records (matrices precomputed once per
+// object instead of per ray as in primitives.rs:303,421,522,628).
+void lower_scene(const rrte_scene_ir* s, std::vector<DPrim>& prims, std::vector<DMaterial>& mats,
+                 std::vector<DLight>& lights) {
+    prims.assign(s->num_prims, DPrim{});
     for (uint32_t i = 0; i < s->num_prims; ++i) {
         const rrte_prim& in = s->prims[i];
         DPrim& o = prims[i];
@@ -240,12 +240,12 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         to_affine12(m, o.xf);
         to_affine12(inv, o.inv);
     }
-    std::vector<DMaterial> mats(s->num_materials);
+    mats.assign(s->num_materials, DMaterial{});
     for (uint32_t i = 0; i < s->num_materials; ++i) {
         static_assert(sizeof(rrte_material) == sizeof(DMaterial), "material layout");
         memcpy(&mats[i], &s->materials[i], sizeof(DMaterial));
     }
-    std::vector<DLight> lights(s->num_lights);
+    lights.assign(s->num_lights, DLight{});
     for (uint32_t i = 0; i < s->num_lights; ++i) {
         const rrte_light& in = s->lights[i];
         DLight& o = lights[i];
@@ -262,6 +262,32 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         memcpy(o.color, in.color, sizeof o.color);
         for (int k = 0; k < 4; ++k) o.cI[k] = in.color[k] * in.intensity;  // Color * f32 (light.rs:189)
     }
+}
+
+// Upload the scene if it differs from the cached copy (the analogue of
+// caching on Scene::is_dirty, crates/rrte-scene/src/lib.rs:310-312).
+rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
+    const size_t bp = sizeof(rrte_prim) * s->num_prims, bm = sizeof(rrte_material) * s->num_materials,
+                 bl = sizeof(rrte_light) * s->num_lights, bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
+    const size_t key_len = bp + bm + bl + bn + 4 * sizeof(uint32_t);
+    bool same = c->scene_key.size() == key_len;
+    if (same) {
+        const unsigned char* k = c->scene_key.data();
+        same = (bp == 0 || !memcmp(k, s->prims, bp)) && (bm == 0 || !memcmp(k + bp, s->materials, bm)) &&
+               (bl == 0 || !memcmp(k + bp + bm, s->lights, bl)) &&
+               (bn == 0 || !memcmp(k + bp + bm + bl, s->sdf_nodes, bn));
+    }
+    *upload_ms = 0.0;
+    if (same) {
+        ++c->same_scene_renders;
+        return RRTE_OK;
+    }
+    c->same_scene_renders = 0;
+
+    std::vector<DPrim> prims;
+    std::vector<DMaterial> mats;
+    std::vector<DLight> lights;
+    lower_scene(s, prims, mats, lights);
     rrte_status r;
     if ((r = ensure(c, c->d_prims, c->cap_prims, prims.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_mats, c->cap_mats, mats.size())) != RRTE_OK) return r;
@@ -279,6 +305,10 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, c->ev2, c->ev0);
     *upload_ms = ms;
+    c->h_prims = prims;
+    c->h_mats = mats;
+    c->h_lights = lights;
+    c->h_nodes.assign(s->sdf_nodes, s->sdf_nodes + s->num_sdf_nodes);
     c->n_prims = s->num_prims;
     c->n_mats = s->num_materials;
     c->n_lights = s->num_lights;
@@ -326,6 +356,8 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     float m[16];
     mat4_srt(trs, m);
     to_affine12(m, k.cam_xf);
+    const char* dbg = getenv("RRTE_DEBUG");  // ablation bits for profiling only
+    k.debug = dbg ? (uint32_t)strtoul(dbg, nullptr, 0) : 0u;
     return k;
 }
 
@@ -339,12 +371,54 @@ uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank
     return rows;
 }
 
+// Scene-specialised kernel for the cached scene + mode, compiling it if the
+// JIT policy says so; nullptr = use the generic kernel.
+constexpr uint32_t kJitMaxPrims = 128, kJitMaxNodes = 1024;
+
+JitKernel* jit_kernel_for(rrte_ctx* c, int mode) {
+    if (c->jit_mode == RRTE_JIT_OFF) return nullptr;
+    if (c->h_prims.size() > kJitMaxPrims || c->h_nodes.size() > kJitMaxNodes) return nullptr;
+    std::string key(c->scene_key.begin(), c->scene_key.end());
+    key.push_back((char)mode);
+    auto it = c->jit_cache.find(key);
+    if (it != c->jit_cache.end()) return it->second.fn ? &it->second : nullptr;
+    if (!(c->jit_mode == RRTE_JIT_ON || c->same_scene_renders >= 1)) return nullptr;
+    if (c->jit_cache.size() >= 32) {
+        for (auto& kv : c->jit_cache) jit_release(kv.second);
+        c->jit_cache.clear();
+    }
+    std::string src = jit_source(c->h_prims.data(), (uint32_t)c->h_prims.size(), c->h_mats.data(),
+                                 (uint32_t)c->h_mats.size(), c->h_lights.data(), (uint32_t)c->h_lights.size(),
+                                 c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode);
+    JitKernel jk;
+    std::string log;
+    if (hipSetDevice(c->device) != hipSuccess || !jit_compile(src, jk, log)) {
+        c->jit_log = log;  // stay on the generic kernel for this scene
+        jk = JitKernel{};
+    } else {
+        c->stats.jit_compile_ms = jk.compile_ms;
+    }
+    auto& slot = c->jit_cache[key];
+    slot = jk;
+    return slot.fn ? &slot : nullptr;
+}
+
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
                    uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     KParams k = make_params(c, s, p, rows);
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, s->num_prims, s->num_lights, s->num_materials};
     dim3 grid((p->width + 15) / 16, (rows + 15) / 16), block(256);
     if (rows == 0) return RRTE_OK;
+    // specialised kernels are single-sample, single-bounce (see ray_color<SINGLE>)
+    const bool single = p->samples_per_pixel == 1 && (p->mode == RRTE_MODE_LAMBERT_SHADOW || p->max_depth <= 1);
+    JitKernel* jk = single ? jit_kernel_for(c, (int)p->mode) : nullptr;
+    c->stats.jit_active = jk ? 1u : 0u;
+    if (jk) {
+        unsigned long long* ctr = c->d_counters;
+        void* args[] = {&k, &d_rgba, &d_f32, &ctr};
+        HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, 1, 256, 1, 1, 0, st, args, nullptr));
+        return RRTE_OK;
+    }
     if (p->mode == RRTE_MODE_REFCOMPAT)
         hipLaunchKernelGGL(ray_kernel<RRTE_MODE_REFCOMPAT>, grid, block, 0, st, k, sv, d_rgba, d_f32, c->d_counters);
     else
@@ -414,6 +488,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     rrte_ctx* c = new (std::nothrow) rrte_ctx();
     if (!c) return RRTE_HIP_ERROR;
     c->device = device;
+    if (const char* j = getenv("RRTE_JIT")) c->jit_mode = (int)strtol(j, nullptr, 0);
     auto bail = [&](hipError_t e) {
         (void)e;
         rrte_hip_destroy(c);
@@ -438,6 +513,7 @@ void rrte_hip_destroy(rrte_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    for (auto& kv : c->jit_cache) jit_release(kv.second);
     void* bufs[] = {c->d_prims, c->d_mats, c->d_lights, c->d_nodes, c->d_rgba,
                     c->d_f32,   c->d_counters, c->d_gather, c->d_full};
     for (void* b : bufs)
@@ -491,10 +567,33 @@ rrte_status rrte_hip_synchronize(rrte_ctx* c) {
     return finish_frame(c);
 }
 
+rrte_status rrte_hip_set_jit(rrte_ctx* c, int mode) {
+    if (!c) return RRTE_INVALID_ARG;
+    if (mode < RRTE_JIT_OFF || mode > RRTE_JIT_AUTO) return fail(c, RRTE_INVALID_ARG, "unknown JIT mode %d", mode);
+    c->jit_mode = mode;
+    return RRTE_OK;
+}
+
 rrte_status rrte_hip_stats(rrte_ctx* c, rrte_stats* out) {
     if (!c || !out) return RRTE_INVALID_ARG;
     *out = c->stats;
     return RRTE_OK;
+}
+
+rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size_t log_len) {
+    if (!s || (s->num_prims && !s->prims) || (s->num_sdf_nodes && !s->sdf_nodes)) return RRTE_INVALID_ARG;
+    std::vector<DPrim> prims;
+    std::vector<DMaterial> mats;
+    std::vector<DLight> lights;
+    lower_scene(s, prims, mats, lights);
+    std::string src = jit_source(prims.data(), (uint32_t)prims.size(), mats.data(), (uint32_t)mats.size(),
+                                 lights.data(), (uint32_t)lights.size(), s->sdf_nodes, s->num_sdf_nodes, mode);
+    std::string msg;
+    bool ok = jit_compile_only(src, msg);
+    if (log && log_len) {
+        snprintf(log, log_len, "%s", ok ? "" : msg.c_str());
+    }
+    return ok ? RRTE_OK : RRTE_HIP_ERROR;
 }
 
 uint32_t rrte_hip_band_rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank) {

@@ -803,7 +803,7 @@ class LoweredScene:
 class Context:
     """Owns one rrte_ctx (one HIP device, its stream and HBM scene cache)."""
 
-    def __init__(self, device: int | None = None):
+    def __init__(self, device: int | None = None, jit: int | None = None):
         self.lib = abi.load()
         if device is None:
             device = int(os.environ.get("RRTE_HIP_DEVICE", "0"))
@@ -812,6 +812,8 @@ class Context:
         if st != abi.RRTE_OK:
             raise abi.RrteError(st, f"rrte_hip_create(device={device}) failed")
         self.h = h
+        if jit is not None:
+            self.check(self.lib.rrte_hip_set_jit(self.h, int(jit)))
 
     def check(self, st):
         if st != abi.RRTE_OK:
@@ -837,9 +839,11 @@ class Context:
 class Raytracer:
     """Raytracer (raytracer.rs:28-149), rendering on an MI355X."""
 
-    def __init__(self, config: RaytracerConfig | None = None, device: int | None = None):
+    def __init__(self, config: RaytracerConfig | None = None, device: int | None = None, jit: int | None = None):
+        """jit: abi.JIT_OFF / JIT_ON / JIT_AUTO (None = library default, AUTO)."""
         self.config = config or RaytracerConfig()
         self._device = device
+        self._jit = jit
         self._ctx: Context | None = None
 
     @staticmethod
@@ -852,7 +856,7 @@ class Raytracer:
     @property
     def ctx(self) -> Context:
         if self._ctx is None:
-            self._ctx = Context(self._device)
+            self._ctx = Context(self._device, self._jit)
         return self._ctx
 
     def render(self, objects, lights, materials, camera: Camera) -> np.ndarray:

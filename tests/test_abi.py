@@ -50,6 +50,17 @@ def test_null_arguments_are_rejected_without_a_device():
     lib.rrte_hip_destroy(None)  # no-op
 
 
+@pytest.mark.parametrize("name", ["sdf-showcase", "deformation-stress", "sdf-showcase-literal"])
+def test_scene_specialised_kernel_source_compiles(name):
+    """jit.hip: the generated per-scene HIP source compiles with hiprtc for gfx950 (no device needed)."""
+    from rrte_amd import LoweredScene, scenes
+    objs, lights, cam, cfg = scenes.SCENES[name](32, 18)
+    sc = LoweredScene(objs, lights, cam)
+    log = C.create_string_buffer(1 << 16)
+    st = abi.load().rrte_hip_jit_check(sc.ref(), 1, log, len(log))
+    assert st == abi.RRTE_OK, log.value.decode()[:4000]
+
+
 def test_create_reports_no_device_off_gpu():
     import torch
     if torch.cuda.is_available():

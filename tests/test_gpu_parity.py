@@ -21,8 +21,8 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-4
 
 
-def compare(objs, lights, cam, cfg, linear_exact=True, threads=16):
-    rt = Raytracer(cfg, device=0)
+def compare(objs, lights, cam, cfg, linear_exact=True, threads=16, jit=abi.JIT_OFF):
+    rt = Raytracer(cfg, device=0, jit=jit)
     g8, gf = rt.render_f32(objs, lights, [], cam)
     st = rt.stats()
     _, glin = rt.render_f32(objs, lights, [], cam, linear=True)
@@ -40,6 +40,8 @@ def compare(objs, lights, cam, cfg, linear_exact=True, threads=16):
     assert u8 <= 1, info
     assert int(st.shadow_rays) == rsh, info
     assert st.primary_rays == cfg.width * cfg.height * cfg.samples_per_pixel
+    single = cfg.samples_per_pixel == 1 and (cfg.mode == "lambert_shadow" or cfg.max_depth <= 1)
+    assert st.jit_active == (1 if (jit == abi.JIT_ON and single) else 0), "unexpected kernel path"
     if linear_exact:
         assert np.array_equal(glin.view(np.uint32), rlin.view(np.uint32)), info
     return info
@@ -65,10 +67,17 @@ def test_golden_fixtures_on_gpu(name, mode, w, h):
     assert hashlib.sha256(lin.tobytes()).hexdigest() == str(fx["linear_sha256"])
 
 
-def test_sdf_showcase_full_1080p():
-    """BASELINE configs[1] at full size (the bench workload)."""
-    info = compare(*scenes.sdf_showcase(1920, 1080))
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+def test_sdf_showcase_full_1080p(jit):
+    """BASELINE configs[1] at full size (the bench workload), generic and scene-specialised kernels."""
+    info = compare(*scenes.sdf_showcase(1920, 1080), jit=jit)
     print(info)
+
+
+@pytest.mark.parametrize("name,mode", SCENE_CASES)
+def test_scene_specialised_kernels_match_oracle(name, mode):
+    """The hiprtc-specialised kernel (jit.hip) must reproduce the oracle exactly like the generic one."""
+    compare(*scenes.SCENES[name](160, 90, mode=mode), jit=abi.JIT_ON)
 
 
 def test_advanced_demo_full_1080p():
@@ -81,16 +90,18 @@ def test_basic_demo_reference_cpu_config_640x480():
     compare(*scenes.basic_demo(640, 480, mode="refcompat"))
 
 
-def test_deformation_stress_4k():
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+def test_deformation_stress_4k(jit):
     """BASELINE configs[4] workload on one GPU (64-node CSG + bend/twist/noise, 3840x2160)."""
-    compare(*scenes.deformation_stress(3840, 2160), threads=16)
+    compare(*scenes.deformation_stress(3840, 2160), threads=16, jit=jit)
 
 
 @pytest.mark.parametrize("fn", [se.mixed_scene, se.all_lights_scene, se.deformers_scene, se.ortho_scene])
 @pytest.mark.parametrize("mode", ["refcompat", "lambert_shadow"])
-def test_extra_scenes(fn, mode):
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+def test_extra_scenes(fn, mode, jit):
     # spot lights use acosf (libm vs device ocml): allow an ulp in the linear image there
-    compare(*fn(200, 120, mode), linear_exact=fn is not se.all_lights_scene)
+    compare(*fn(200, 120, mode), linear_exact=fn is not se.all_lights_scene, jit=jit)
 
 
 def test_stochastic_multibounce_materials():
@@ -117,9 +128,25 @@ def test_empty_scene_no_lights_depth0_and_no_material():
     compare(objs, lights, cam, cfg)
 
 
+def test_jit_auto_policy_specialises_on_second_frame():
+    objs, lights, cam, cfg = scenes.sdf_showcase(96, 54)
+    rt = Raytracer(cfg, device=0, jit=abi.JIT_AUTO)
+    a = rt.render(objs, lights, [], cam)
+    assert rt.stats().jit_active == 0
+    b = rt.render(objs, lights, [], cam)
+    st = rt.stats()
+    assert st.jit_active == 1 and st.jit_compile_ms > 0
+    assert np.array_equal(a, b)
+    cam.transform.position = (cam.transform.position[0], cam.transform.position[1] + np.float32(0.5),
+                              cam.transform.position[2])
+    c = rt.render(objs, lights, [], cam)  # camera motion: no recompile, still specialised
+    assert rt.stats().jit_active == 1 and not np.array_equal(a, c)
+    compare(objs, lights, cam, cfg)
+
+
 def test_scene_cache_invalidates_on_change():
     objs, lights, cam, cfg = scenes.sdf_showcase(96, 54)
-    rt = Raytracer(cfg, device=0)
+    rt = Raytracer(cfg, device=0, jit=abi.JIT_OFF)
     a = rt.render(objs, lights, [], cam)
     b = rt.render(objs, lights, [], cam)
     assert np.array_equal(a, b)

@@ -6,13 +6,14 @@ by 2x on gfx950 (doubled here, flagged as uncalibrated for this access pattern);
 is exact for wide stores; both are per dispatch.
 """
 import collections
+import re
 import csv
 import json
 import sys
 from pathlib import Path
 
 src, name, workload = Path(sys.argv[1]), sys.argv[2], sys.argv[3]
-KERNEL = "ray_kernel"
+KERNEL_RE = re.compile(r"ray_kernel|rrte_jit_kernel")
 out_md = [f"# rocprofv3 summary: {name}", "", f"workload: `{workload}`", ""]
 stats = src / "trace" / "run_kernel_stats.csv"
 if stats.exists():
@@ -21,7 +22,7 @@ pmc = collections.defaultdict(list)
 meta = {}
 for f in sorted(src.glob("pmc*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if KERNEL in r["Kernel_Name"]:
+        if KERNEL_RE.search(r["Kernel_Name"]):
             pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                       "Scratch_Size", "VGPR_Count", "SGPR_Count")}
@@ -29,7 +30,7 @@ avg = {k: sum(v) / len(v) for k, v in pmc.items()}
 dur_ns = None
 if stats.exists():
     for r in csv.DictReader(open(stats)):
-        if KERNEL in r["Name"]:
+        if KERNEL_RE.search(r["Name"]):
             dur_ns = float(r["AverageNs"])
 res = {"workload": workload, "kernel": meta.get("Kernel_Name"), "dispatch": meta, "counters_per_dispatch": avg,
        "avg_kernel_ns": dur_ns}
