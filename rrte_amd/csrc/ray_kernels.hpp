@@ -13,6 +13,8 @@
 namespace rrte {
 
 constexpr float kInf = __builtin_huge_valf();
+constexpr uint32_t kCounterShards = 256;  // shadow-ray counter shards (power of two)
+constexpr uint32_t kCounterStride = 16;   // u64 per shard: one 128-B line each
 
 // Runtime scene: device pointers + counts (the generic kernel).  A
 // scene-specialised kernel (jit.cpp, hiprtc) instead passes a struct whose
@@ -988,7 +990,12 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
         uint32_t v = nshadow;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0 && v) atomicAdd(counters, (unsigned long long)v);
+        // 256 counter shards, one 128-B line each: same-address atomics from
+        // every wave of the grid would serialise at the memory side.
+        if (lane == 0 && v) {
+            const uint32_t shard = (blockIdx.x + blockIdx.y * gridDim.x + threadIdx.x / 64u * 61u) & (kCounterShards - 1u);
+            atomicAdd(counters + shard * kCounterStride, (unsigned long long)v);
+        }
     }
 }
 

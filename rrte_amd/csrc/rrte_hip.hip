@@ -40,8 +40,8 @@ struct rrte_ctx {
     // frame buffers for the blocking entry points
     uint32_t* d_rgba = nullptr; size_t cap_rgba = 0;
     float4* d_f32 = nullptr; size_t cap_f32 = 0;
-    unsigned long long* d_counters = nullptr;   // [0] shadow rays (accumulating)
-    unsigned long long* h_counters = nullptr;   // pinned
+    unsigned long long* d_counters = nullptr;   // shadow rays, kCounterShards x kCounterStride (accumulating)
+    unsigned long long* h_counters = nullptr;   // pinned copy
     unsigned long long shadow_base = 0;         // value at the start of the last frame
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -64,6 +64,8 @@ struct rrte_ctx {
 };
 
 namespace {
+
+constexpr size_t kCounterBytes = sizeof(unsigned long long) * kCounterShards * kCounterStride;
 
 rrte_status fail(rrte_ctx* c, rrte_status st, const char* fmt, ...) {
     if (c) {
@@ -429,10 +431,12 @@ rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params
 
 // Read back the device counters and close the frame's statistics.
 rrte_status finish_frame(rrte_ctx* c) {
-    HIPCHK(c, hipMemcpyAsync(c->h_counters, c->d_counters, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->stats.shadow_rays = c->h_counters[0] - c->shadow_base;
-    c->shadow_base = c->h_counters[0];
+    unsigned long long total = 0;
+    for (uint32_t i = 0; i < kCounterShards; ++i) total += c->h_counters[i * kCounterStride];
+    c->stats.shadow_rays = total - c->shadow_base;
+    c->shadow_base = total;
     if (c->pending_kernel_timing) {
         float ms = 0.0f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->stats.kernel_ms = ms;
@@ -500,10 +504,10 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail(e);
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail(e);
     if ((e = hipEventCreate(&c->ev2)) != hipSuccess) return bail(e);
-    if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), 2 * sizeof(unsigned long long))) != hipSuccess) return bail(e);
-    if ((e = hipMemset(c->d_counters, 0, 2 * sizeof(unsigned long long))) != hipSuccess) return bail(e);
-    if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_counters), 2 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess) return bail(e);
-    c->h_counters[0] = c->h_counters[1] = 0;
+    if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), kCounterBytes)) != hipSuccess) return bail(e);
+    if ((e = hipMemset(c->d_counters, 0, kCounterBytes)) != hipSuccess) return bail(e);
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_counters), kCounterBytes, hipHostMallocDefault)) != hipSuccess) return bail(e);
+    memset(c->h_counters, 0, kCounterBytes);
     *out = c;
     return RRTE_OK;
 }
