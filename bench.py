@@ -86,7 +86,8 @@ def pmc_traffic(workload_key):
         except Exception:
             continue
         if d.get("workload") == workload_key and d.get("hbm_bytes_per_launch") is not None:
-            best = d
+            if best is None or d.get("created", 0) >= best.get("created", 0):
+                best = d
     return best
 
 

@@ -10,6 +10,7 @@ import re
 import csv
 import json
 import sys
+import time
 from pathlib import Path
 
 src, name, workload = Path(sys.argv[1]), sys.argv[2], sys.argv[3]
@@ -32,7 +33,7 @@ if stats.exists():
     for r in csv.DictReader(open(stats)):
         if KERNEL_RE.search(r["Name"]):
             dur_ns = float(r["AverageNs"])
-res = {"workload": workload, "kernel": meta.get("Kernel_Name"), "dispatch": meta, "counters_per_dispatch": avg,
+res = {"created": time.time(), "workload": workload, "kernel": meta.get("Kernel_Name"), "dispatch": meta, "counters_per_dispatch": avg,
        "avg_kernel_ns": dur_ns}
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     fetch = avg["FETCH_SIZE"] * 1024 * 2  # gfx950: FETCH_SIZE reads 1/2 of wide coalesced reads
