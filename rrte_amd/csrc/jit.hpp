@@ -17,9 +17,9 @@ struct JitKernel {
 };
 
 // HIP source for one scene + shading mode: the scene as static constexpr arrays
-// and an extern "C" rrte_jit_kernel instantiating ray_kernel_body<mode, Scene>.
+// and an extern "C" rrte_jit_kernel instantiating ray_kernel_body<mode, Scene, true, cull>.
 std::string jit_source(const DPrim* prims, uint32_t np, const DMaterial* mats, uint32_t nm, const DLight* lights,
-                       uint32_t nl, const rrte_sdf_node* nodes, uint32_t nn, int mode);
+                       uint32_t nl, const rrte_sdf_node* nodes, uint32_t nn, int mode, bool cull);
 
 // hiprtc compile for gfx950 + module load.  On failure `log` holds the reason.
 bool jit_compile(const std::string& src, JitKernel& out, std::string& log);

@@ -683,15 +683,100 @@ __device__ __forceinline__ int closest_hit(const S& sc, const Ray& r, float t_mi
 
 // Any hit in [t_min, t_max] (LAMBERT_SHADOW shadow rays).
 template <class S>
-__device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min, float t_max) {
-    bool hit_any = false, all_done = false;
+__device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min, float t_max, uint64_t mask) {
+    bool hit_any = false;
     for_each_prim(sc, [&](auto ii) {
-        if (all_done) return;  // wave-uniform: every active lane already occluded
+        const uint32_t i = ii;
+        // one wave-uniform skip test: culled, or every lane already occluded (mask cleared)
+        if (mask == 0 || (i < 64u && !((mask >> i) & 1ull))) return;
         Hit h;
         if (!hit_any && intersect_at<false>(sc, ii, r, t_min, t_max, h)) hit_any = true;
-        all_done = __all(hit_any);
+        if (__all(hit_any)) mask = 0;
     });
     return hit_any;
+}
+
+// --------------------------------------------------------------- culling
+// Shadow-ray culling.  Conservative per-object bounding spheres (host-
+// computed, inflated; radius +inf = never culled) let a wave drop the objects
+// none of its shadow rays towards a light can reach.  The 64 object tests run
+// lane-parallel (lane j tests object j) and __ballot turns them into a
+// wave-uniform candidate mask, so occluded() skips culled objects with scalar
+// branches.  An object that is not culled runs its exact intersector: culling
+// never changes a result.  (Culling primary rays against the tile's view cone
+// was measured too and did not pay: a miss is already a cheap bound test.)
+struct Cull {
+    const float4* __restrict__ bounds;  // one per object; nullptr = culling off
+    uint32_t n;                         // objects with a bound (culling needs n <= 64)
+};
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ bool finite3(f3 a) {
+    return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
+}
+__device__ __forceinline__ bool cull_on(const Cull& cl) { return cl.bounds != nullptr && cl.n <= 64u; }
+
+// Bounding sphere of the wave's shading points (lanes with `hit`).
+// `ext` = the lane's shadow-origin offset |n|*bias (normals need not be unit).
+struct HitBound { f3 c; float r, ext; bool any, unsafe; };
+__device__ __forceinline__ HitBound wave_hit_bound(bool hit, f3 p, f3 n, float bias) {
+    const bool use = hit && finite3(p) && finite3(n);
+    const float ext = bias * vlen(n);
+    float lx = wave_min(use ? p.x : kInf), ly = wave_min(use ? p.y : kInf), lz = wave_min(use ? p.z : kInf);
+    float hx = wave_max(use ? p.x : -kInf), hy = wave_max(use ? p.y : -kInf), hz = wave_max(use ? p.z : -kInf);
+    HitBound b;
+    b.any = lx <= hx;
+    b.unsafe = __any(hit && !use);
+    b.c = V((lx + hx) * 0.5f, (ly + hy) * 0.5f, (lz + hz) * 0.5f);
+    f3 d = V(hx - lx, hy - ly, hz - lz);
+    b.r = 0.5f * __builtin_sqrtf(vdot(d, d));
+    b.ext = wave_max(use ? ext : 0.0f);
+    return b;
+}
+
+// Shadow rays of one light: every ray runs from within `hb` (grown by the
+// origin offset) to the light (point/spot; the segment ends at the light plus
+// the same offset) or towards -direction (directional), so all of them lie in
+// the capsule of radius hb.r + hb.ext around the axis from hb.c.  Waves with
+// a non-finite hit point or normal, and directional lights whose direction is
+// not unit length (the sphere tracer's bound test assumes |d| = 1), are not
+// culled.  Wave-uniform inputs only: call with all 64 lanes active.
+__device__ __forceinline__ uint64_t shadow_cull(const Cull& cl, const HitBound& hb, const DLight& l) {
+    if (!cull_on(cl) || hb.unsafe || l.kind == RRTE_LIGHT_AMBIENT) return ~0ull;
+    if (!hb.any) return 0ull;
+    const bool directional = l.kind == RRTE_LIGHT_DIRECTIONAL;
+    const f3 ld = V(l.direction[0], l.direction[1], l.direction[2]);
+    if (directional && !(fabsf(vdot(ld, ld) - 1.0f) <= 1e-3f)) return ~0ull;
+    const f3 A = hb.c;
+    const f3 B = directional ? vsub(A, ld) : V(l.position[0], l.position[1], l.position[2]);
+    const f3 AB = vsub(B, A);
+    const float ab2 = vdot(AB, AB);
+    const float scale = fmaxf(fmaxf(fabsf(A.x), fabsf(A.y)), fmaxf(fabsf(A.z), fmaxf(fmaxf(fabsf(B.x), fabsf(B.y)), fabsf(B.z))));
+    const float R = hb.r + hb.ext + 1e-3f + 1e-4f * scale;
+    const uint32_t j = threadIdx.x & 63u;
+    bool cand = false;
+    if (j < cl.n) {
+        const float4 b = cl.bounds[j];
+        cand = true;
+        if (__builtin_isfinite(b.w) && ab2 > 0.0f) {
+            f3 P = V(b.x, b.y, b.z);
+            float t = vdot(vsub(P, A), AB) / ab2;
+            t = directional ? fmaxf(t, 0.0f) : clampf_(t, 0.0f, 1.0f);
+            f3 q = vsub(P, vadd(A, vmuls(AB, t)));
+            float rr = R + b.w;
+            cand = vdot(q, q) <= rr * rr * 1.0001f;
+        }
+    }
+    return __ballot(cand);
 }
 
 // --------------------------------------------------------------- lighting
@@ -829,12 +914,21 @@ __device__ __forceinline__ Ray generate_ray(const KParams& kp, float u, float v)
 // evaluated forward with a running albedo product; that is bit-identical to
 // the recursion for max_depth <= 2 (the parity configs use 1) and differs by
 // rounding only beyond.
-// SINGLE (scene-specialised kernels): exactly one bounce -- the host only
-// selects it when max_depth == 1 or the mode is LAMBERT_SHADOW -- so the
-// kernel is straight-line code apart from the march loops.
-template <int MODE, class S, bool SINGLE>
-__device__ __forceinline__ Col ray_color(const S& sc, const KParams& kp, Ray r, uint32_t& st,
-                                         uint32_t& nshadow) {
+// Material record of a hit (nullptr = no material -> BLACK, raytracer.rs:139-143).
+template <class S>
+__device__ __forceinline__ const DMaterial* material_of(const S& sc, int idx) {
+    const int mi = sc.prims[idx].material;
+    return (mi < 0 || (uint32_t)mi >= sc.num_materials) ? nullptr : &sc.mats[mi];
+}
+
+// REFCOMPAT: Raytracer::ray_color (raytracer.rs:92-148) for one camera ray:
+// ambient + sum(light.color*I*att) + albedo * ray_color(scatter).  The
+// reference recursion color_d = local_d + albedo_d * color_{d+1} is evaluated
+// forward with a running albedo product: bit-identical to the recursion for
+// max_depth <= 2 (the parity configs use 1), rounding-level beyond.
+// SINGLE (scene-specialised kernels): one bounce only (max_depth == 1).
+template <class S, bool SINGLE>
+__device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray r, uint32_t& st) {
     Col out{0.0f, 0.0f, 0.0f, 1.0f};
     if (kp.max_depth == 0) return out;
     float tr = 1.0f, tg = 1.0f, tb = 1.0f;  // running albedo product
@@ -852,52 +946,21 @@ __device__ __forceinline__ Col ray_color(const S& sc, const KParams& kp, Ray r, 
             }
             break;
         }
-        if (kp.debug & 2u) {  // primary visibility only
-            out = Col{h.t * 0.01f, 0.0f, 0.0f, 1.0f};
-            break;
-        }
-        const DPrim& pr = sc.prims[idx];
-        int mi = pr.material;
-        if (mi < 0 || (uint32_t)mi >= sc.num_materials) break;  // BLACK
-        const DMaterial& m = sc.mats[mi];
-        float ar = m.albedo[0], ag = m.albedo[1], ab = m.albedo[2], aa = m.albedo[3];
+        const DMaterial* m = material_of(sc, idx);
+        if (!m) break;  // BLACK
+        float ar = m->albedo[0], ag = m->albedo[1], ab = m->albedo[2], aa = m->albedo[3];
         // BLACK + ambient_color()*0.1 (raytracer.rs:124, material.rs:10-12)
         float cr = 0.0f + (ar * 0.1f) * 0.1f;
         float cg = 0.0f + (ag * 0.1f) * 0.1f;
         float cb = 0.0f + (ab * 0.1f) * 0.1f;
         float ca = 1.0f + (aa * 0.1f) * 0.1f;
-        if (MODE == RRTE_MODE_REFCOMPAT) {
-            for_each_light(sc, [&](auto lii) {
-                Contrib k = illuminate(light_at(sc, lii), h.p);
-                cr = cr + k.cr * k.att;
-                cg = cg + k.cg * k.att;
-                cb = cb + k.cb * k.att;
-                ca = ca + k.ca * k.att;
-            });
-        } else {
-            const float bias = kp.bias;
-            for_each_light(sc, [&](auto lii) {
-                const auto& l = light_at(sc, lii);
-                Contrib k = illuminate(l, h.p);
-                if (l.kind == RRTE_LIGHT_AMBIENT) {
-                    cr = cr + ar * k.cr;
-                    cg = cg + ag * k.cg;
-                    cb = cb + ab * k.cb;
-                    return;
-                }
-                float ndl = vdot(h.n, k.dir);
-                if (ndl > 0.0f && k.att > 0.0f) {
-                    ++nshadow;
-                    Ray sr = ray_new(vadd(h.p, vmuls(h.n, bias)), k.dir);
-                    if ((kp.debug & 1u) || !occluded(sc, sr, bias, k.dist)) {
-                        float f = k.att * ndl;
-                        cr = cr + ar * (k.cr * f);
-                        cg = cg + ag * (k.cg * f);
-                        cb = cb + ab * (k.cb * f);
-                    }
-                }
-            });
-        }
+        for_each_light(sc, [&](auto lii) {
+            Contrib k = illuminate(light_at(sc, lii), h.p);
+            cr = cr + k.cr * k.att;
+            cg = cg + k.cg * k.att;
+            cb = cb + k.cb * k.att;
+            ca = ca + k.ca * k.att;
+        });
         if (depth == 0) {
             out = Col{cr, cg, cb, ca};
         } else {
@@ -905,9 +968,8 @@ __device__ __forceinline__ Col ray_color(const S& sc, const KParams& kp, Ray r, 
             out.g = out.g + tg * cg;
             out.b = out.b + tb * cb;
         }
-        if (MODE != RRTE_MODE_REFCOMPAT) break;  // direct lighting only
         Ray sc_ray;
-        if (!scatter(m, r, h, st, sc_ray)) break;
+        if (!scatter(*m, r, h, st, sc_ray)) break;
         if (depth == 0) out.a = out.a + 1.0f;  // Color::from(Vec3) has alpha 1 (color.rs:78-82)
         if (depth + 1 >= kp.max_depth) break;   // ray_color(depth 0) == BLACK: adds 0
         tr = tr * ar;
@@ -915,6 +977,79 @@ __device__ __forceinline__ Col ray_color(const S& sc, const KParams& kp, Ray r, 
         tb = tb * ab;
         r = sc_ray;
     }
+    return out;
+}
+
+// LAMBERT_SHADOW (build-defined) for one camera ray.  Called by
+// all 64 lanes of the wave (`live` marks the lanes that own a pixel): with
+// CULL the hit-point bound and the per-light shadow culls are wave reductions.
+template <class S, bool CULL>
+__device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, const Cull& cl, const Ray& r, bool live,
+                                             uint32_t& nshadow) {
+    Col out{0.0f, 0.0f, 0.0f, 1.0f};
+    if (kp.max_depth == 0) return out;
+    Hit h;
+    const int idx = closest_hit(sc, r, live ? kp.t_min : kInf, h);  // idle lanes find nothing
+    const DMaterial* m = idx >= 0 ? material_of(sc, idx) : nullptr;
+    const bool hit = m != nullptr;
+    if (idx < 0) out = Col{kp.bg[0], kp.bg[1], kp.bg[2], kp.bg[3]};
+    if (kp.debug & 2u) {  // diagnostics: primary visibility only
+        if (idx >= 0) out = Col{h.t * 0.01f, 0.0f, 0.0f, 1.0f};
+        return out;
+    }
+    float ar = 0.0f, ag = 0.0f, ab = 0.0f, cr = 0.0f, cg = 0.0f, cb = 0.0f, ca = 1.0f;
+    if (hit) {
+        ar = m->albedo[0]; ag = m->albedo[1]; ab = m->albedo[2];
+        // BLACK + ambient_color()*0.1 (raytracer.rs:124, material.rs:10-12)
+        cr = 0.0f + (ar * 0.1f) * 0.1f;
+        cg = 0.0f + (ag * 0.1f) * 0.1f;
+        cb = 0.0f + (ab * 0.1f) * 0.1f;
+        ca = 1.0f + (m->albedo[3] * 0.1f) * 0.1f;
+    }
+    const float bias = kp.bias;
+    // contribution of one light to a hit lane (light.rs illuminate + N.L + shadow ray)
+    auto shade = [&](const DLight& l, uint64_t smask) {
+        Contrib k = illuminate(l, h.p);
+        if (l.kind == RRTE_LIGHT_AMBIENT) {
+            cr = cr + ar * k.cr;
+            cg = cg + ag * k.cg;
+            cb = cb + ab * k.cb;
+            return;
+        }
+        const float ndl = vdot(h.n, k.dir);
+        if (ndl > 0.0f && k.att > 0.0f) {
+            ++nshadow;
+            Ray sr = ray_new(vadd(h.p, vmuls(h.n, bias)), k.dir);
+            if ((kp.debug & 1u) || !occluded(sc, sr, bias, k.dist, smask)) {
+                float f = k.att * ndl;
+                cr = cr + ar * (k.cr * f);
+                cg = cg + ag * (k.cg * f);
+                cb = cb + ab * (k.cb * f);
+            }
+        }
+    };
+    if constexpr (!CULL) {
+        if (hit) for_each_light(sc, [&](auto lii) { shade(light_at(sc, lii), ~0ull); });
+    } else {
+        HitBound hb{};
+        hb.unsafe = true;  // no bounds table: every mask all-ones
+        if (cull_on(cl)) hb = wave_hit_bound(hit, h.p, h.n, bias);
+        if constexpr (S::kStatic) {
+            // all light masks first, at one converged point, then the shading
+            uint64_t smask[S::num_lights ? S::num_lights : 1];
+            auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii)); };
+            auto shade_one = [&](auto lii) { if (hit) shade(light_at(sc, lii), smask[(uint32_t)lii]); };
+            static_for<0, S::num_lights>(cull_one);
+            static_for<0, S::num_lights>(shade_one);
+        } else {
+#pragma unroll 1
+            for (uint32_t li = 0; li < sc.num_lights; ++li) {
+                const uint64_t sm = shadow_cull(cl, hb, sc.lights[li]);
+                if (hit) shade(sc.lights[li], sm);
+            }
+        }
+    }
+    if (hit) out = Col{cr, cg, cb, ca};
     return out;
 }
 
@@ -938,36 +1073,46 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
     return (b * kp.nranks + kp.rank) * kp.band_rows + w;
 }
 
-// One lane per pixel; wave = 8x8 tile, workgroup = 16x16 pixels.
-template <int MODE, class S, bool SINGLE = false>
-__device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, uint32_t* __restrict__ out_rgba8,
-                                                float4* __restrict__ out_f32,
+// One lane per pixel; wave = 8x8 tile, workgroup = 16x16 pixels.  Every lane
+// of a wave runs the sample loop (lanes past the image edge are idle but
+// present) so the culling reductions see converged waves.  CULL selects the
+// shadow-culled LAMBERT_SHADOW variant (the host picks it per scene).
+template <int MODE, class S, bool SINGLE = false, bool CULL = false>
+__device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, const Cull& cl,
+                                                uint32_t* __restrict__ out_rgba8, float4* __restrict__ out_f32,
                                                 unsigned long long* __restrict__ counters) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t lr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const bool live = x < kp.width && lr < kp.rows;
+    const uint32_t xc = live ? x : 0u;
+    const uint32_t y = image_row(kp, live ? lr : 0u);
+    const uint32_t pix = y * kp.width + xc;
     uint32_t nshadow = 0;
-    if (x < kp.width && lr < kp.rows) {
-        const uint32_t y = image_row(kp, lr);
-        const uint32_t pix = y * kp.width + x;
-        Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
-        const uint32_t nsamples = SINGLE ? 1u : kp.spp;
-        for (uint32_t s = 0; s < nsamples; ++s) {
-            uint32_t st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
-            float jx = 0.5f, jy = 0.5f;
-            if (kp.jitter == RRTE_JITTER_RANDOM) {
-                jx = rng_f32(st);
-                jy = rng_f32(st);
-            }
-            float u = ((float)x + jx) / (float)kp.width;
-            float v = ((float)y + jy) / (float)kp.height;
-            Ray r = generate_ray(kp, u, v);
-            Col c = ray_color<MODE, S, SINGLE>(sc, kp, r, st, nshadow);
-            acc.r = acc.r + c.r;
-            acc.g = acc.g + c.g;
-            acc.b = acc.b + c.b;
-            acc.a = acc.a + c.a;
+    Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
+    const uint32_t nsamples = SINGLE ? 1u : kp.spp;
+    for (uint32_t s = 0; s < nsamples; ++s) {
+        uint32_t st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
+        float jx = 0.5f, jy = 0.5f;
+        if (kp.jitter == RRTE_JITTER_RANDOM) {
+            jx = rng_f32(st);
+            jy = rng_f32(st);
         }
+        float u = ((float)xc + jx) / (float)kp.width;
+        float v = ((float)y + jy) / (float)kp.height;
+        Ray r = generate_ray(kp, u, v);
+        Col c{0.0f, 0.0f, 0.0f, 1.0f};
+        if (MODE == RRTE_MODE_LAMBERT_SHADOW) {
+            c = shade_lambert<S, CULL>(sc, kp, cl, r, live, nshadow);
+        } else if (live) {
+            c = ray_color_ref<S, SINGLE>(sc, kp, r, st);
+        }
+        acc.r = acc.r + c.r;
+        acc.g = acc.g + c.g;
+        acc.b = acc.b + c.b;
+        acc.a = acc.a + c.a;
+    }
+    if (live) {
         acc.r = acc.r * kp.inv_spp;
         acc.g = acc.g * kp.inv_spp;
         acc.b = acc.b * kp.inv_spp;
@@ -1000,11 +1145,11 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
 }
 
 // Generic kernel: the scene is read from HBM through wave-uniform (scalar) loads.
-template <int MODE>
-__global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, uint32_t* __restrict__ out_rgba8,
+template <int MODE, bool CULL>
+__global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, Cull cl, uint32_t* __restrict__ out_rgba8,
                                                   float4* __restrict__ out_f32,
                                                   unsigned long long* __restrict__ counters) {
-    ray_kernel_body<MODE, SceneView>(kp, sc, out_rgba8, out_f32, counters);
+    ray_kernel_body<MODE, SceneView, false, CULL>(kp, sc, cl, out_rgba8, out_f32, counters);
 }
 
 // Root-side de-interleave after the RCCL gather: the gathered buffer holds

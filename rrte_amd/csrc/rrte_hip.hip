@@ -36,6 +36,7 @@ struct rrte_ctx {
     DMaterial* d_mats = nullptr; size_t cap_mats = 0;
     DLight* d_lights = nullptr; size_t cap_lights = 0;
     rrte_sdf_node* d_nodes = nullptr; size_t cap_nodes = 0;
+    float4* d_bounds = nullptr; size_t cap_bounds = 0;  // culling spheres, one per object
     uint32_t n_prims = 0, n_mats = 0, n_lights = 0, n_nodes = 0;
     // frame buffers for the blocking entry points
     uint32_t* d_rgba = nullptr; size_t cap_rgba = 0;
@@ -219,11 +220,67 @@ rrte_status validate(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_para
     return RRTE_OK;
 }
 
+// Conservative world-space bounding sphere of one object for wave culling
+// (ray_kernels.hpp, primary_cull/shadow_cull): every point the object's
+// intersector can report lies inside it.  Radius +inf = never culled (planes,
+// non-finite data).  Computed in double and inflated, so f32 rounding in the
+// intersectors stays inside.
+float4 prim_bound(const rrte_prim& in, const DPrim& d) {
+    const double inf = __builtin_huge_val();
+    double c[3] = {in.p[0], in.p[1], in.p[2]}, r = inf;
+    bool local = true;  // bound given in object space (transformed below)
+    switch (in.kind) {
+    case RRTE_PRIM_SPHERE: r = fabs((double)in.p[3]); local = false; break;
+    case RRTE_PRIM_TRIANGLE: {
+        for (int k = 0; k < 3; ++k) c[k] = ((double)in.p[k] + in.p[3 + k] + in.p[6 + k]) / 3.0;
+        r = 0.0;
+        for (int v = 0; v < 3; ++v) {
+            double dx = in.p[3 * v] - c[0], dy = in.p[3 * v + 1] - c[1], dz = in.p[3 * v + 2] - c[2];
+            r = fmax(r, sqrt(dx * dx + dy * dy + dz * dz));
+        }
+        local = false;
+        break;
+    }
+    case RRTE_PRIM_CUBE: {
+        double sx = in.p[4], sy = in.p[5], sz = in.p[6];
+        r = 0.5 * sqrt(sx * sx + sy * sy + sz * sz);
+        break;
+    }
+    case RRTE_PRIM_CYLINDER:
+    case RRTE_PRIM_CONE: {
+        double rad = in.p[3], hh = 0.5 * in.p[4];
+        r = sqrt(rad * rad + hh * hh);
+        break;
+    }
+    case RRTE_PRIM_CAPSULE: r = 0.5 * fabs((double)in.p[4]) + fabs((double)in.p[3]); break;
+    case RRTE_PRIM_SDF: r = fabs((double)in.p[3]); local = false; break;  // the sphere tracer's own bound
+    default: break;                                                       // plane: unbounded
+    }
+    if (local && r < inf) {  // p' = M p: centre through xf, radius by the largest column norm
+        double w[3];
+        for (int k = 0; k < 3; ++k)
+            w[k] = (double)d.xf[0 + k] * c[0] + (double)d.xf[3 + k] * c[1] + (double)d.xf[6 + k] * c[2] + d.xf[9 + k];
+        double sn = 0.0;
+        for (int col = 0; col < 3; ++col) {
+            double a = d.xf[col * 3], b = d.xf[col * 3 + 1], e = d.xf[col * 3 + 2];
+            sn = fmax(sn, sqrt(a * a + b * b + e * e));
+        }
+        r *= sn * (1.0 + 1e-5);  // M = R*S (mat4_srt): orthogonal columns, so |M v| <= max column norm * |v|
+        c[0] = w[0]; c[1] = w[1]; c[2] = w[2];
+    }
+    double mag = fmax(fabs(c[0]), fmax(fabs(c[1]), fabs(c[2])));
+    r = r * 1.001 + 1e-3 + 1e-5 * mag;
+    if (!(r < 3e38) || !std::isfinite(c[0]) || !std::isfinite(c[1]) || !std::isfinite(c[2]))
+        return make_float4(0.0f, 0.0f, 0.0f, __builtin_huge_valf());
+    return make_float4((float)c[0], (float)c[1], (float)c[2], nextafterf((float)r, __builtin_huge_valf()));
+}
+
 // Lower the ABI records to device records (matrices precomputed once per
 // object instead of per ray as in primitives.rs:303,421,522,628).
 void lower_scene(const rrte_scene_ir* s, std::vector<DPrim>& prims, std::vector<DMaterial>& mats,
-                 std::vector<DLight>& lights) {
+                 std::vector<DLight>& lights, std::vector<float4>* bounds = nullptr) {
     prims.assign(s->num_prims, DPrim{});
+    if (bounds) bounds->assign(s->num_prims, float4{});
     for (uint32_t i = 0; i < s->num_prims; ++i) {
         const rrte_prim& in = s->prims[i];
         DPrim& o = prims[i];
@@ -241,6 +298,7 @@ void lower_scene(const rrte_scene_ir* s, std::vector<DPrim>& prims, std::vector<
         mat4_inverse(m, inv);
         to_affine12(m, o.xf);
         to_affine12(inv, o.inv);
+        if (bounds) (*bounds)[i] = prim_bound(in, o);
     }
     mats.assign(s->num_materials, DMaterial{});
     for (uint32_t i = 0; i < s->num_materials; ++i) {
@@ -289,9 +347,11 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     std::vector<DPrim> prims;
     std::vector<DMaterial> mats;
     std::vector<DLight> lights;
-    lower_scene(s, prims, mats, lights);
+    std::vector<float4> bounds;
+    lower_scene(s, prims, mats, lights, &bounds);
     rrte_status r;
     if ((r = ensure(c, c->d_prims, c->cap_prims, prims.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, c->d_bounds, c->cap_bounds, bounds.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_mats, c->cap_mats, mats.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_lights, c->cap_lights, lights.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_nodes, c->cap_nodes, (size_t)s->num_sdf_nodes)) != RRTE_OK) return r;
@@ -300,6 +360,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     if (!mats.empty()) HIPCHK(c, hipMemcpyAsync(c->d_mats, mats.data(), mats.size() * sizeof(DMaterial), hipMemcpyHostToDevice, st));
     if (!lights.empty()) HIPCHK(c, hipMemcpyAsync(c->d_lights, lights.data(), lights.size() * sizeof(DLight), hipMemcpyHostToDevice, st));
     if (bn) HIPCHK(c, hipMemcpyAsync(c->d_nodes, s->sdf_nodes, bn, hipMemcpyHostToDevice, st));
+    if (!bounds.empty()) HIPCHK(c, hipMemcpyAsync(c->d_bounds, bounds.data(), bounds.size() * sizeof(float4), hipMemcpyHostToDevice, st));
     // the staging vectors die at return: make the copies complete first
     HIPCHK(c, hipStreamSynchronize(st));
     HIPCHK(c, hipEventRecord(c->ev0, st));
@@ -373,15 +434,28 @@ uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank
     return rows;
 }
 
+// Shadow-ray culling (ray_kernels.hpp, shadow_cull) for LAMBERT_SHADOW frames: one lane per object,
+// so scenes of <= 64 objects; it pays where an occlusion test is expensive (sphere-traced SDF
+// objects) and costs a few percent on all-analytic scenes (measured).  RRTE_CULL=0/1
+// forces it off/on (A/B runs, tests).
+bool cull_policy(const rrte_scene_ir* s, uint32_t mode) {
+    if (mode != RRTE_MODE_LAMBERT_SHADOW || s->num_prims > 64) return false;
+    if (const char* ce = getenv("RRTE_CULL")) return ce[0] != '0';
+    for (uint32_t i = 0; i < s->num_prims; ++i)
+        if (s->prims[i].kind == RRTE_PRIM_SDF) return true;
+    return false;
+}
+
 // Scene-specialised kernel for the cached scene + mode, compiling it if the
 // JIT policy says so; nullptr = use the generic kernel.
 constexpr uint32_t kJitMaxPrims = 128, kJitMaxNodes = 1024;
 
-JitKernel* jit_kernel_for(rrte_ctx* c, int mode) {
+JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull) {
     if (c->jit_mode == RRTE_JIT_OFF) return nullptr;
     if (c->h_prims.size() > kJitMaxPrims || c->h_nodes.size() > kJitMaxNodes) return nullptr;
     std::string key(c->scene_key.begin(), c->scene_key.end());
     key.push_back((char)mode);
+    key.push_back((char)cull);
     auto it = c->jit_cache.find(key);
     if (it != c->jit_cache.end()) return it->second.fn ? &it->second : nullptr;
     if (!(c->jit_mode == RRTE_JIT_ON || c->same_scene_renders >= 1)) return nullptr;
@@ -391,7 +465,7 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode) {
     }
     std::string src = jit_source(c->h_prims.data(), (uint32_t)c->h_prims.size(), c->h_mats.data(),
                                  (uint32_t)c->h_mats.size(), c->h_lights.data(), (uint32_t)c->h_lights.size(),
-                                 c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode);
+                                 c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull);
     JitKernel jk;
     std::string log;
     if (hipSetDevice(c->device) != hipSuccess || !jit_compile(src, jk, log)) {
@@ -409,22 +483,26 @@ rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params
                    uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     KParams k = make_params(c, s, p, rows);
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, s->num_prims, s->num_lights, s->num_materials};
+    const bool cull = cull_policy(s, p->mode);
+    Cull cl{cull ? c->d_bounds : nullptr, s->num_prims};
     dim3 grid((p->width + 15) / 16, (rows + 15) / 16), block(256);
     if (rows == 0) return RRTE_OK;
     // specialised kernels are single-sample, single-bounce (see ray_color<SINGLE>)
     const bool single = p->samples_per_pixel == 1 && (p->mode == RRTE_MODE_LAMBERT_SHADOW || p->max_depth <= 1);
-    JitKernel* jk = single ? jit_kernel_for(c, (int)p->mode) : nullptr;
+    JitKernel* jk = single ? jit_kernel_for(c, (int)p->mode, cull) : nullptr;
     c->stats.jit_active = jk ? 1u : 0u;
     if (jk) {
         unsigned long long* ctr = c->d_counters;
-        void* args[] = {&k, &d_rgba, &d_f32, &ctr};
+        void* args[] = {&k, &cl, &d_rgba, &d_f32, &ctr};
         HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, 1, 256, 1, 1, 0, st, args, nullptr));
         return RRTE_OK;
     }
     if (p->mode == RRTE_MODE_REFCOMPAT)
-        hipLaunchKernelGGL(ray_kernel<RRTE_MODE_REFCOMPAT>, grid, block, 0, st, k, sv, d_rgba, d_f32, c->d_counters);
+        hipLaunchKernelGGL((ray_kernel<RRTE_MODE_REFCOMPAT, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
+    else if (cull)
+        hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, true>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     else
-        hipLaunchKernelGGL(ray_kernel<RRTE_MODE_LAMBERT_SHADOW>, grid, block, 0, st, k, sv, d_rgba, d_f32, c->d_counters);
+        hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     HIPCHK(c, hipGetLastError());
     return RRTE_OK;
 }
@@ -518,7 +596,7 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto& kv : c->jit_cache) jit_release(kv.second);
-    void* bufs[] = {c->d_prims, c->d_mats, c->d_lights, c->d_nodes, c->d_rgba,
+    void* bufs[] = {c->d_prims, c->d_mats, c->d_lights, c->d_nodes, c->d_bounds, c->d_rgba,
                     c->d_f32,   c->d_counters, c->d_gather, c->d_full};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -591,7 +669,8 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
     std::vector<DLight> lights;
     lower_scene(s, prims, mats, lights);
     std::string src = jit_source(prims.data(), (uint32_t)prims.size(), mats.data(), (uint32_t)mats.size(),
-                                 lights.data(), (uint32_t)lights.size(), s->sdf_nodes, s->num_sdf_nodes, mode);
+                                 lights.data(), (uint32_t)lights.size(), s->sdf_nodes, s->num_sdf_nodes, mode,
+                                 cull_policy(s, (uint32_t)mode));
     std::string msg;
     bool ok = jit_compile_only(src, msg);
     if (log && log_len) {

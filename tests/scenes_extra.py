@@ -73,3 +73,31 @@ def ortho_scene(w, h, mode):
     cam = Camera.new_orthographic(-4, 4, -3, 3, 0.1, 100.0)
     cam.transform.position = vec3(0, 2, 10)
     return objs, lights, cam, cfg
+
+
+def cull_stress_scene(w, h, mode, n_spheres=40, seed=7):
+    """Shadow-culling edge cases: many small close objects casting grazing shadows, transformed
+    analytic prims, a plane with a NON-unit normal (shadow origins offset by |n|*bias), a
+    directional light with a non-unit direction, a point light inside the object cloud."""
+    import random
+    rnd = random.Random(seed)
+    mats = [LambertianMaterial(Color.rgb(0.3 + 0.6 * rnd.random(), 0.3 + 0.6 * rnd.random(), 0.3 + 0.6 * rnd.random()))
+            for _ in range(4)]
+    objs = [Plane((0, 0, 0), (0, 2.5, 0), mats[0])]
+    for i in range(n_spheres):
+        objs.append(Sphere((rnd.uniform(-4, 4), rnd.uniform(0.2, 2.5), rnd.uniform(-4, 4)), rnd.uniform(0.08, 0.35),
+                           mats[i % 4]))
+    cube = Cube((0.0, 0.6, 0.0), (0.8, 0.5, 1.2), mats[1])
+    cube.transform = Transform(position=(0.5, 0.1, -0.5), rotation=(0.0, 0.38268343, 0.0, 0.92387953), scale=(1.5, 1, 0.7))
+    objs += [cube, Cylinder((2.5, 0.8, 2.0), 0.3, 1.2, mats[2]), Cone((-2.5, 0.8, 2.0), 0.5, 1.0, mats[3]),
+             Capsule((0.0, 0.5, 3.0), 0.25, 0.6, mats[1]), Triangle((-3, 0.05, -4), (3, 0.05, -4), (0, 2.5, -4), mats[2]),
+             SDFObject(SDFTorus((2.0, 1.5, -2.0), 0.6, 0.2), mats[3])]
+    lights = [PointLight((0.3, 1.5, 0.2), Color.rgb(1, 0.9, 0.8), 1.5),
+              DirectionalLight((-0.6, -2.0, -0.4), Color(1.0, 0.95, 0.8, 1.0), 0.5),
+              SpotLight((0, 6, 0), (0, -1, 0), Color.rgb(0.6, 0.8, 1.0), 5.0, 0.4, 0.8)]
+    cam = Camera.new_perspective(to_radians(55.0), f32(w) / f32(h), 0.1, 100.0)
+    cam.transform.position = vec3(5, 4, 7)
+    cam.look_at((0, 1, 0))
+    cfg = RaytracerConfig(max_depth=1, samples_per_pixel=1, width=w, height=h, jitter="center", mode=mode,
+                          background_color=Color(0.1, 0.1, 0.15, 1))
+    return objs, lights, cam, cfg

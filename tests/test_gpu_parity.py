@@ -104,6 +104,32 @@ def test_extra_scenes(fn, mode, jit):
     compare(*fn(200, 120, mode), linear_exact=fn is not se.all_lights_scene, jit=jit)
 
 
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+@pytest.mark.parametrize("case", ["cull_stress", "cull_stress_66", "mixed", "all_lights", "advanced-demo",
+                                  "sdf-showcase", "deformers"])
+def test_shadow_culling_is_exact(case, jit, monkeypatch):
+    """Shadow-ray culling (RRTE_CULL forces it on/off regardless of the scene policy) never changes
+    a bit: culled and unculled renders are identical (linear image and shadow-ray count), and both
+    match the oracle.  cull_stress_66 has > 64 objects, where culling must switch itself off."""
+    if case.startswith("cull_stress"):
+        args = se.cull_stress_scene(240, 160, "lambert_shadow", n_spheres=60 if case.endswith("66") else 40)
+    elif case in ("mixed", "all_lights", "deformers"):
+        args = getattr(se, case + "_scene")(200, 120, "lambert_shadow")
+    else:
+        args = scenes.SCENES[case](320, 180)
+    objs, lights, cam, cfg = args
+    out = {}
+    for cull in ("0", "1"):
+        monkeypatch.setenv("RRTE_CULL", cull)
+        # spot lights use acosf (libm vs device ocml): an ulp in the linear image vs the oracle
+        compare(*args, linear_exact=case not in ("all_lights", "cull_stress", "cull_stress_66"), jit=jit)
+        rt = Raytracer(cfg, device=0, jit=jit)
+        _, lin = rt.render_f32(objs, lights, [], cam, linear=True)
+        out[cull] = (lin.view(np.uint32).copy(), int(rt.stats().shadow_rays))
+    assert np.array_equal(out["0"][0], out["1"][0])
+    assert out["0"][1] == out["1"][1]
+
+
 def test_stochastic_multibounce_materials():
     """Reference default workload shape: spp > 1, random jitter, depth > 1, Lambertian/Metal/
     Dielectric/Emissive scatter (§8f rank 1).  Same counter-based RNG stream on both sides;
