@@ -42,39 +42,72 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-stock", action="store_true", help="skip the stock-config secondary measurement")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
 
 
-def cpu_baseline(scene, params, budget_s):
-    """The oracle (C restatement of Raytracer::render) on this host's cores, whole frames,
-    median over frames within the time budget (1 warm-up frame)."""
-    import oracle
-
+def cpu_threads():
     threads = int(os.environ.get("RRTE_CPU_THREADS", os.cpu_count() or 1))
     # the GPU box shows the whole machine in os.cpu_count(); our share is what sched_getaffinity allows
     try:
         threads = min(threads, len(os.sched_getaffinity(0)))
     except AttributeError:
         pass
-    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    return min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+
+
+def cpu_baseline(scene, params, budget_s, stock=None):
+    """The oracle (C restatement of Raytracer::render) on this host's cores (SURVEY §8d):
+    N threads: median of up to 5 whole frames after 1 warm-up; 1 thread: one whole frame (or a
+    row band if the budget is short); plus the reference's stock config on a row band."""
+    import oracle
+
+    threads = cpu_threads()
+    W, H = params.width, params.height
     oracle.render(scene, params, nthreads=threads, want_f32=False)  # warm-up
     times, shadow = [], 0
     t_start = time.perf_counter()
-    while True:
+    while len(times) < 5:
         t0 = time.perf_counter()
         _, _, shadow = oracle.render(scene, params, nthreads=threads, want_f32=False)
         times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > budget_s or len(times) >= 25:
+        if time.perf_counter() - t_start > budget_s:
             break
     med = statistics.median(times)
-    rays = params.width * params.height * params.samples_per_pixel + shadow
-    return {
+    rays = W * H * params.samples_per_pixel + shadow
+    out = {
         "value": rays / med / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
-        "sample": f"{len(times)} whole {params.width}x{params.height} frames of the same scene/mode, median "
+        "sample": f"median of {len(times)} whole {W}x{H} frames (1 warm-up) of the same scene/mode, "
                   f"{med * 1e3:.1f} ms/frame, oracle/rrte_oracle.c -O3 -march=x86-64-v3, {threads} threads",
     }
+    # 1 thread: whole frame if it fits the budget (estimated from the N-thread time), else a centre band
+    est = med * threads
+    rows = (0, H) if est <= budget_s else (H // 2 - max(8, int(H * budget_s / est)) // 2,
+                                          H // 2 + max(8, int(H * budget_s / est)) // 2)
+    t0 = time.perf_counter()
+    _, _, sh1 = oracle.render(scene, params, nthreads=1, rows=rows, want_f32=False)
+    t1 = time.perf_counter() - t0
+    out["single_thread"] = {"value": (W * (rows[1] - rows[0]) * params.samples_per_pixel + sh1) / t1 / 1e6,
+                            "unit": "Mray/s", "cores": 1, "rows": list(rows)}
+    if stock is not None:  # reference stock config (spp 4, depth 50, random jitter/scatter) on a row band
+        sscene, sprm, band = stock
+        t0 = time.perf_counter()
+        oracle.render(sscene, sprm, nthreads=threads, rows=band, want_f32=False)
+        ts = time.perf_counter() - t0
+        out["stock_config"] = {"value": W * (band[1] - band[0]) * sprm.samples_per_pixel / ts / 1e6,
+                               "unit": "Msample/s", "cores": threads, "rows": list(band)}
+    return out
+
+
+def flop_tally(scene, params):
+    """Algorithmic FP32 ops of one frame from the oracle's instrumented counting build
+    (oracle/rrte_oracle.c rrte_oracle_flops).  Not timed."""
+    import oracle
+
+    cnt, flops = oracle.count(scene, params, nthreads=cpu_threads())
+    return flops, int(cnt.sdf_steps), int(cnt.samples + cnt.shadow_rays)
 
 
 def pmc_traffic(workload_key):
@@ -89,6 +122,14 @@ def pmc_traffic(workload_key):
             if best is None or d.get("created", 0) >= best.get("created", 0):
                 best = d
     return best
+
+
+def stock_config(args):
+    """The reference's own default workload on the same scene (SURVEY §8d secondary number):
+    REFCOMPAT, spp 4, max_depth 50, random jitter and scatter (counter-based RNG)."""
+    objs, lights, cam, cfg = scenes.SCENES[args.scene](args.width, args.height, mode="refcompat")
+    cfg.samples_per_pixel, cfg.max_depth, cfg.jitter = 4, 50, "random"
+    return LoweredScene(objs, lights, cam), cfg.lower()
 
 
 def main():
@@ -175,6 +216,42 @@ def main():
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
         primary, shadow = int(cnt[0].item()), int(cnt[1].item())
 
+    # single-frame latency (enqueue -> frame complete on the device), D2H of the frame separately
+    lat = []
+    for _ in range(5):
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        a = time.perf_counter()
+        step()
+        torch.cuda.synchronize(dev)
+        lat.append(time.perf_counter() - a)
+    latency_ms = statistics.median(lat) * 1e3
+    host = torch.empty(W * H, dtype=torch.int32, pin_memory=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    host.copy_(full, non_blocking=True)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    d2h_ms = e0.elapsed_time(e1)
+
+    # the reference's stock config on the generic kernel (rank 0, N=1 only; not the headline)
+    stock = None
+    if world == 1 and not args.no_stock:
+        sscene, sprm = stock_config(args)
+        for _ in range(2):
+            ctx.check(lib.rrte_hip_render_async(ctx.h, sscene.ref(), C.byref(sprm), full.data_ptr(), None, sptr))
+        torch.cuda.synchronize(dev)
+        n_stock = 5
+        a = time.perf_counter()
+        for _ in range(n_stock):
+            ctx.check(lib.rrte_hip_render_async(ctx.h, sscene.ref(), C.byref(sprm), full.data_ptr(), None, sptr))
+        torch.cuda.synchronize(dev)
+        ts = (time.perf_counter() - a) / n_stock
+        stock = {"workload": f"{args.scene} {W}x{H} reference stock config: REFCOMPAT, spp=4, max_depth=50, "
+                             "random jitter + scatter (counter-based RNG)",
+                 "value": round(W * H * 4 / ts / 1e6, 3), "unit": "Msample/s", "ms_per_frame": round(ts * 1e3, 4)}
+
     if rank == 0:
         rays = primary + shadow
         value = rays / elapsed / 1e6
@@ -222,11 +299,28 @@ def main():
                 "note": "VALU-bound path (no dense contraction, no MFMA); HBM traffic is the 4 B/pixel frame store",
             },
         }
+        line["primary_only"] = {"value": round(primary / elapsed / 1e6, 3), "unit": "Mray/s"}
+        line["frame_latency_ms"] = round(latency_ms, 4)
+        line["d2h_ms"] = round(d2h_ms, 4)  # frame to pinned host memory, excluded from `value`
         if pmc and pmc.get("valu") is not None:
             line["valu"] = pmc["valu"]
+        if stock is not None:
+            line["stock_config"] = stock
         if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(scene, prm, args.cpu_seconds)
+            flops, _, _ = flop_tally(scene, prm)
+            tf = flops / (avg_launch_ms * 1e-3) / 1e12
+            line["valu_roofline"] = {
+                "bound": "valu-fp32", "flops_per_frame": flops, "achieved": round(tf, 3), "unit": "TFLOP/s",
+                "peak": VALU_PEAK_TFLOPS, "frac": tf / VALU_PEAK_TFLOPS,
+                "frac_of_unpacked_peak": tf / (VALU_PEAK_TFLOPS / 2),
+                "note": "algorithmic FP32 ops from the oracle's instrumented counting build (SURVEY §8d) / "
+                        "avg kernel duration; peak = packed-FP32 vector peak (the kernel issues unpacked FP32)"}
+            sband = (H // 2 - H // 8, H // 2 + H // 8)  # centre quarter of the frame
+            line["cpu_baseline"] = cpu_baseline(scene, prm, args.cpu_seconds,
+                                                stock=(*stock_config(args), sband) if stock else None)
             line["cpu_baseline"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 2)
+            if stock and "stock_config" in line["cpu_baseline"]:
+                line["stock_config"]["gpu_over_cpu"] = round(stock["value"] / line["cpu_baseline"]["stock_config"]["value"], 2)
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist_on:

@@ -86,3 +86,48 @@ def render(scene, params, nthreads=None, rows=None, want_f32=True, linear=False)
     if st != 0:
         raise ValueError(f"oracle rejected the scene/params (status {st})")
     return out8, outf, sh.value
+
+
+class Counts(C.Structure):
+    """Mirror of rrte_oracle_counts (rrte_oracle.h)."""
+    _fields_ = [("samples", C.c_uint64), ("pixels", C.c_uint64), ("isect_calls", C.c_uint64 * 8),
+                ("isect_hits", C.c_uint64 * 8), ("root_checks", C.c_uint64), ("sdf_steps", C.c_uint64),
+                ("sdf_normals", C.c_uint64), ("sdf_nodes", C.c_uint64 * 128), ("noise_octaves", C.c_uint64),
+                ("light_evals", C.c_uint64 * 4), ("shaded_hits", C.c_uint64), ("lambert_lights", C.c_uint64),
+                ("shadow_rays", C.c_uint64), ("lambert_terms", C.c_uint64), ("ref_light_terms", C.c_uint64),
+                ("scatters", C.c_uint64 * 4), ("sphere_samples", C.c_uint64)]
+
+
+_clib = None
+
+
+def load_counting():
+    """The counting build (librrte_oracle_count.so): same source, event counters compiled in."""
+    global _clib
+    if _clib is not None:
+        return _clib
+    path = _HERE / "build" / "librrte_oracle_count.so"
+    if not path.exists():
+        build()
+    lib = C.CDLL(str(path))
+    lib.rrte_oracle_render_counted.restype = C.c_int
+    lib.rrte_oracle_render_counted.argtypes = [C.POINTER(abi.SceneIR), C.POINTER(abi.RenderParams),
+                                               C.POINTER(Counts), C.c_int, C.c_uint32, C.c_uint32]
+    lib.rrte_oracle_flops.restype = C.c_double
+    lib.rrte_oracle_flops.argtypes = [C.POINTER(Counts)]
+    _clib = lib
+    return lib
+
+
+def count(scene, params, nthreads=None, rows=None):
+    """Instrumented event counts of one render and their algorithmic FP32 op total
+    (SURVEY.md §8d).  Returns (Counts, flops)."""
+    lib = load_counting()
+    prm = abi.RenderParams.from_buffer_copy(params)
+    cnt = Counts()
+    r0, r1 = rows if rows else (0, 0)
+    if nthreads is None:
+        nthreads = int(os.environ.get("RRTE_ORACLE_THREADS", os.cpu_count() or 1))
+    if lib.rrte_oracle_render_counted(C.byref(scene.ir), C.byref(prm), C.byref(cnt), nthreads, r0, r1) != 0:
+        raise ValueError("oracle rejected the scene/params")
+    return cnt, float(lib.rrte_oracle_flops(C.byref(cnt)))

@@ -23,6 +23,14 @@
 /* ------------------------------------------------------------ glam Vec3 */
 typedef struct v3 { float x, y, z; } v3;
 
+/* Event counters (counting build only, see rrte_oracle.h). */
+#ifdef RRTE_ORACLE_COUNT
+static _Thread_local rrte_oracle_counts* tl_cnt;
+#define CNT(f) (++tl_cnt->f)
+#else
+#define CNT(f) ((void)0)
+#endif
+
 static inline v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
 static inline v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
 static inline v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -368,6 +376,7 @@ static v3 sdf_deform(const rrte_sdf_node* n, v3 p) {
             float amp = 1.0f, fr = 1.0f, sum = 0.0f;
             for (uint32_t o = 0; o < oct; ++o) {
                 uint32_t sd = seed + (uint32_t)k * 0x9e3779b9u + o * 0x85ebca6bu;
+                CNT(noise_octaves);
                 sum = sum + amp * rrte_oracle_value_noise(x.x * fr, x.y * fr, x.z * fr, sd);
                 amp = amp * f[5];
                 fr = fr * 2.0f;
@@ -397,6 +406,7 @@ static float sdf_eval(const rrte_sdf_node* nodes, uint32_t count, v3 p) {
     for (uint32_t i = 0; i < count; ++i) {
         const rrte_sdf_node* n = &nodes[i];
         uint32_t op = n->op;
+        CNT(sdf_nodes[op & 127u]);
         if (op < 32) {
             vs[sp++] = sdf_leaf(n, p);
         } else if (op < 64) {
@@ -468,9 +478,12 @@ static int sdf_intersect(const octx* c, const rrte_prim* pr, const ray* r, float
     if (t > tend) return 0;
     float eps = pr->sdf_hit_eps, scale = pr->sdf_step_scale;
     for (uint32_t i = 0; i < pr->sdf_max_steps; ++i) {
+        CNT(sdf_steps);
         v3 p = ray_at(r, t);
         float d = sdf_obj_eval(c, pr, p);
         if (d < eps * t) {
+            CNT(sdf_normals);
+            CNT(isect_hits[RRTE_PRIM_SDF]);
             /* tetrahedral normal estimate, h = 1e-3 */
             const float h = 1e-3f;
             float f0 = sdf_obj_eval(c, pr, V(p.x + h, p.y - h, p.z - h));
@@ -496,6 +509,7 @@ static inline void local_ray(const rrte_prim* pr, const ray* r, ray* lr, float m
 
 /* SceneObject::intersect dispatch (primitives.rs:57-725). */
 static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_min, float t_max, hit* out) {
+    CNT(isect_calls[pr->kind & 7u]);
     switch (pr->kind) {
     case RRTE_PRIM_SPHERE: { /* primitives.rs:57-81 */
         v3 ctr = vload(pr->p);
@@ -513,6 +527,7 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
             if (root < t_min || t_max < root) return 0;
         }
         v3 p = ray_at(r, root);
+        CNT(isect_hits[pr->kind & 7u]);
         *out = hit_new(root, p, vdivs(vsub(p, ctr), rad), r);
         return 1;
     }
@@ -523,6 +538,7 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
         float t = vdot(vsub(pt, r->o), n) / denom;
         if (t < t_min || t > t_max) return 0;
         v3 p = ray_at(r, t);
+        CNT(isect_hits[pr->kind & 7u]);
         *out = hit_new(t, p, denom < 0.0f ? n : vneg(n), r);
         return 1;
     }
@@ -545,6 +561,7 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
         float w = 1.0f - u - v;
         v3 n0 = vload(pr->p + 9), n1 = vload(pr->p + 12), n2 = vload(pr->p + 15);
         v3 n = vnorm(vadd(vadd(vmuls(n0, w), vmuls(n1, u)), vmuls(n2, v)));
+        CNT(isect_hits[pr->kind & 7u]);
         *out = hit_new(t, p, n, r);
         return 1;
     }
@@ -577,6 +594,7 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
         float t = (t_near >= t_min) ? t_near : t_far;
         if (t < t_min || t > t_max) return 0;
         v3 lp = ray_at(&lr, t);
+        CNT(isect_hits[pr->kind & 7u]);
         *out = hit_new(t, m4_point(m, lp), vnorm(m4_vector(m, normal)), r);
         return 1;
     }
@@ -597,9 +615,11 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
         for (int k = 0; k < 2; ++k) {
             float t = ts[k];
             if (t >= t_min && t <= t_max) {
+                CNT(root_checks);
                 v3 p = ray_at(&lr, t);
                 if (fabsf(p.y - ctr.y) <= hh) {
                     v3 ln = V((p.x - ctr.x) / rad, 0.0f, (p.z - ctr.z) / rad);
+                    CNT(isect_hits[pr->kind & 7u]);
                     *out = hit_new(t, m4_point(m, p), vnorm(m4_vector(m, ln)), r);
                     return 1;
                 }
@@ -626,11 +646,13 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
         for (int kk = 0; kk < 2; ++kk) {
             float t = ts[kk];
             if (t >= t_min && t <= t_max) {
+                CNT(root_checks);
                 v3 p = ray_at(&lr, t);
                 float yl = p.y - ctr.y;
                 if (yl >= -hh && yl <= hh) {
                     float rr = sqrtf(p.x * p.x + p.z * p.z);
                     v3 ln = vnorm(V(p.x / rr, k, p.z / rr));
+                    CNT(isect_hits[pr->kind & 7u]);
                     *out = hit_new(t, m4_point(m, p), vnorm(m4_vector(m, ln)), r);
                     return 1;
                 }
@@ -661,11 +683,13 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
                 for (int k = 0; k < 2; ++k) {
                     float t = ts[k];
                     if (t >= t_min && t <= t_max && t < closest) {
+                        CNT(root_checks);
                         v3 p = ray_at(&lr, t);
                         int ok = cap == 0 ? (p.y >= ctr.y) : (p.y <= ctr.y);
                         if (ok) {
                             v3 ln = vnorm(vsub(p, cc_));
                             closest = t;
+                            CNT(isect_hits[pr->kind & 7u]);
                             best = hit_new(t, m4_point(m, p), vnorm(m4_vector(m, ln)), r);
                             found = 1;
                         }
@@ -684,10 +708,12 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
             for (int k = 0; k < 2; ++k) {
                 float t = ts[k];
                 if (t >= t_min && t <= t_max && t < closest) {
+                    CNT(root_checks);
                     v3 p = ray_at(&lr, t);
                     if (fabsf(p.y - ctr.y) <= hh) {
                         v3 ln = V((p.x - ctr.x) / rad, 0.0f, (p.z - ctr.z) / rad);
                         closest = t;
+                        CNT(isect_hits[pr->kind & 7u]);
                         best = hit_new(t, m4_point(m, p), vnorm(m4_vector(m, ln)), r);
                         found = 1;
                     }
@@ -720,6 +746,7 @@ static inline float rng_f32(uint32_t* st) {
 }
 static inline v3 rand_in_unit_sphere(uint32_t* st) { /* vector.rs:35-46 */
     for (;;) {
+        CNT(sphere_samples);
         float x = rng_f32(st) * 2.0f - 1.0f;
         float y = rng_f32(st) * 2.0f - 1.0f;
         float z = rng_f32(st) * 2.0f - 1.0f;
@@ -731,6 +758,7 @@ static inline v3 reflect3(v3 v, v3 n) { return vsub(v, vmuls(n, 2.0f * vdot(v, n
 
 /* Material::scatter (material.rs:60-72, 99-110, 147-170, 200-202). Returns 0 for None. */
 static int scatter(const rrte_material* m, const ray* rin, const hit* h, uint32_t* st, ray* out) {
+    CNT(scatters[m->kind & 3u]);
     switch (m->kind) {
     case RRTE_MAT_LAMBERTIAN: {
         v3 sd = vadd(h->n, vnorm(rand_in_unit_sphere(st)));
@@ -812,6 +840,7 @@ typedef struct contrib { col color; v3 dir; float dist, att; } contrib;
 /* Light::illuminate (light.rs:87-94, 182-194, 289-304, 365-372). */
 static contrib illuminate(const rrte_light* l, v3 p) {
     contrib k;
+    CNT(light_evals[l->kind & 3u]);
     k.color = cmuls(cload(l->color), l->intensity);
     switch (l->kind) {
     case RRTE_LIGHT_POINT: {
@@ -862,8 +891,10 @@ static col ray_color(const octx* c, const ray* r, uint32_t depth, uint32_t* st, 
     const rrte_material* m = &c->s->materials[pr->material];
     col alb = cload(m->albedo);
     col color = cadd(BLACK, cmuls(cmuls(alb, 0.1f), 0.1f));
+    CNT(shaded_hits);
     if (c->prm->mode == RRTE_MODE_REFCOMPAT) {
         for (uint32_t i = 0; i < c->s->num_lights; ++i) {
+            CNT(ref_light_terms);
             contrib k = illuminate(&c->s->lights[i], h.p);
             color = cadd(color, cmuls(k.color, k.att));
         }
@@ -885,11 +916,14 @@ static col ray_color(const octx* c, const ray* r, uint32_t depth, uint32_t* st, 
             color.b = color.b + alb.b * k.color.b;
             continue;
         }
+        CNT(lambert_lights);
         float ndl = vdot(h.n, k.dir);
         if (ndl > 0.0f && k.att > 0.0f) {
             ++*nshadow;
+            CNT(shadow_rays);
             ray sr = ray_new(vadd(h.p, vmuls(h.n, bias)), k.dir);
             if (!occluded(c, &sr, bias, k.dist)) {
+                CNT(lambert_terms);
                 float f = k.att * ndl;
                 color.r = color.r + alb.r * (k.color.r * f);
                 color.g = color.g + alb.g * (k.color.g * f);
@@ -917,6 +951,10 @@ typedef struct job {
     uint32_t row_begin, row_end;
     atomic_uint next_row;
     atomic_ullong shadow;
+#ifdef RRTE_ORACLE_COUNT
+    pthread_mutex_t mu;
+    rrte_oracle_counts* counts;
+#endif
 } job;
 
 enum { ROWS_PER_CHUNK = 2 };
@@ -929,7 +967,9 @@ static void render_row(job* jb, uint32_t y, uint64_t* nshadow) {
     for (uint32_t x = 0; x < W; ++x) {
         uint32_t pix = y * W + x;
         col color = BLACK;
+        CNT(pixels);
         for (uint32_t s = 0; s < prm->samples_per_pixel; ++s) {
+            CNT(samples);
             uint32_t st = pcg_hash(pcg_hash(pcg_hash(prm->seed) ^ pix) ^ s);
             float jx = 0.5f, jy = 0.5f;
             if (prm->jitter == RRTE_JITTER_RANDOM) { jx = rng_f32(&st); jy = rng_f32(&st); }
@@ -958,6 +998,11 @@ static void render_row(job* jb, uint32_t y, uint64_t* nshadow) {
 static void* worker(void* arg) {
     job* jb = (job*)arg;
     uint64_t local = 0;
+#ifdef RRTE_ORACLE_COUNT
+    rrte_oracle_counts* mine = (rrte_oracle_counts*)calloc(1, sizeof(rrte_oracle_counts));
+    rrte_oracle_counts scratch;
+    tl_cnt = mine ? mine : &scratch;
+#endif
     for (;;) {
         uint32_t y0 = atomic_fetch_add(&jb->next_row, ROWS_PER_CHUNK);
         if (y0 >= jb->row_end) break;
@@ -965,6 +1010,17 @@ static void* worker(void* arg) {
         for (uint32_t y = y0; y < y1; ++y) render_row(jb, y, &local);
     }
     atomic_fetch_add(&jb->shadow, local);
+#ifdef RRTE_ORACLE_COUNT
+    if (mine) {
+        pthread_mutex_lock(&jb->mu);
+        uint64_t* dst = (uint64_t*)jb->counts;
+        const uint64_t* src = (const uint64_t*)mine;
+        for (size_t i = 0; i < sizeof(rrte_oracle_counts) / sizeof(uint64_t); ++i) dst[i] += src[i];
+        pthread_mutex_unlock(&jb->mu);
+        free(mine);
+    }
+    tl_cnt = NULL;
+#endif
     return NULL;
 }
 
@@ -984,9 +1040,9 @@ static int validate_scene(const rrte_scene_ir* s, const rrte_render_params* p) {
     return 1;
 }
 
-int rrte_oracle_render(const rrte_scene_ir* scene, const rrte_render_params* params,
-                       uint8_t* out_rgba8, float* out_f32, uint64_t* shadow_rays,
-                       int nthreads, uint32_t row_begin, uint32_t row_end) {
+static int render_impl(const rrte_scene_ir* scene, const rrte_render_params* params, uint8_t* out_rgba8,
+                       float* out_f32, uint64_t* shadow_rays, int nthreads, uint32_t row_begin, uint32_t row_end,
+                       rrte_oracle_counts* counts) {
     if (!validate_scene(scene, params)) return 1;
     if (row_begin == 0 && row_end == 0) row_end = params->height;
     if (row_end > params->height || row_begin > row_end) return 1;
@@ -1000,6 +1056,12 @@ int rrte_oracle_render(const rrte_scene_ir* scene, const rrte_render_params* par
     jb->row_end = row_end;
     atomic_init(&jb->next_row, row_begin);
     atomic_init(&jb->shadow, 0);
+#ifdef RRTE_ORACLE_COUNT
+    pthread_mutex_init(&jb->mu, NULL);
+    jb->counts = counts;
+#else
+    (void)counts;
+#endif
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
@@ -1010,9 +1072,32 @@ int rrte_oracle_render(const rrte_scene_ir* scene, const rrte_render_params* par
     worker(jb);
     for (int i = 0; i < started; ++i) pthread_join(th[i], NULL);
     if (shadow_rays) *shadow_rays = atomic_load(&jb->shadow);
+#ifdef RRTE_ORACLE_COUNT
+    pthread_mutex_destroy(&jb->mu);
+#endif
     free(jb);
     return 0;
 }
+
+int rrte_oracle_render(const rrte_scene_ir* scene, const rrte_render_params* params,
+                       uint8_t* out_rgba8, float* out_f32, uint64_t* shadow_rays,
+                       int nthreads, uint32_t row_begin, uint32_t row_end) {
+#ifdef RRTE_ORACLE_COUNT
+    rrte_oracle_counts scratch;
+    memset(&scratch, 0, sizeof scratch);
+    return render_impl(scene, params, out_rgba8, out_f32, shadow_rays, nthreads, row_begin, row_end, &scratch);
+#else
+    return render_impl(scene, params, out_rgba8, out_f32, shadow_rays, nthreads, row_begin, row_end, NULL);
+#endif
+}
+
+#ifdef RRTE_ORACLE_COUNT
+int rrte_oracle_render_counted(const rrte_scene_ir* scene, const rrte_render_params* params,
+                               rrte_oracle_counts* counts, int nthreads, uint32_t row_begin, uint32_t row_end) {
+    if (!counts) return 1;
+    return render_impl(scene, params, NULL, NULL, NULL, nthreads, row_begin, row_end, counts);
+}
+#endif
 
 int rrte_oracle_intersect(const rrte_scene_ir* scene, uint32_t idx, const float o[3], const float d[3],
                           float t_min, float t_max, oracle_hit* out) {
@@ -1031,4 +1116,48 @@ int rrte_oracle_intersect(const rrte_scene_ir* scene, uint32_t idx, const float 
 float rrte_oracle_sdf_eval(const rrte_scene_ir* scene, uint32_t idx, const float p[3]) {
     const rrte_prim* pr = &scene->prims[idx];
     return sdf_eval(scene->sdf_nodes + pr->sdf_first, pr->sdf_count, vload(p));
+}
+
+/* ------------------------------------------------ algorithmic flop tally */
+/* FP32 operations per counted event, tallied from the code above (add, sub, mul,
+ * div, sqrt, min, max and each transcendental = 1; abs, negation and compares = 0).
+ * Analytic object transforms are priced with the inverse precomputed once per
+ * object (as the device does), not rebuilt per ray as primitives.rs:303 does.
+ * Intersector "call" weights price the test up to its usual early exit; the
+ * root/attribute work is priced by the hit and root-check events. */
+double rrte_oracle_flops(const rrte_oracle_counts* c) {
+    if (!c) return 0.0;
+    /* u,v (4) + generate_ray: ndc 4, tan/half 3, scale 2, normalize 10, quat*vec 38, Ray::new 10 (67) + accumulate 4 */
+    const double w_sample = 75.0;
+    const double w_pixel = 11.0;                      /* /spp 4, powf x3, *255 x4 */
+    /*                              sphere plane tri  cube cyl  cone caps  sdf(bound test) */
+    static const double w_call[8] = {23.0, 14.0, 30.0, 146.0, 79.0, 91.0, 133.0, 21.0};
+    static const double w_hit[8] = {22.0, 11.0, 60.0, 54.0, 52.0, 64.0, 60.0, 36.0};
+    const double w_root = 7.0, w_step = 9.0;
+    double w_node[128] = {0};
+    w_node[RRTE_SDF_SPHERE] = 10; w_node[RRTE_SDF_BOX] = 22; w_node[RRTE_SDF_CYLINDER] = 19;
+    w_node[RRTE_SDF_PRISM] = 12; w_node[RRTE_SDF_TORUS] = 13; w_node[RRTE_SDF_TUBE] = 24;
+    w_node[RRTE_SDF_RING] = 13; w_node[RRTE_SDF_CONE] = 38; w_node[RRTE_SDF_CAPSULE] = 14;
+    w_node[RRTE_SDF_ELLIPSOID] = 27;
+    w_node[RRTE_SDF_UNION] = 1; w_node[RRTE_SDF_DIFFERENCE] = 1; w_node[RRTE_SDF_INTERSECTION] = 1;
+    w_node[RRTE_SDF_SMOOTH_UNION] = 13; w_node[RRTE_SDF_SMOOTH_DIFFERENCE] = 13;
+    w_node[RRTE_SDF_SMOOTH_INTERSECTION] = 13;
+    w_node[RRTE_SDF_BEND] = 39; w_node[RRTE_SDF_TWIST] = 39; w_node[RRTE_SDF_TAPER] = 16;
+    w_node[RRTE_SDF_NOISE] = 15; w_node[RRTE_SDF_WAVE] = 35;
+    const double w_octave = 65.0;                     /* scale 3, value noise 58, accumulate 4 */
+    static const double w_light[4] = {29.0, 4.0, 39.0, 4.0};  /* point, directional, spot, ambient */
+    const double w_shaded = 12.0, w_ndl = 5.0, w_shadow = 16.0, w_term = 10.0, w_ref_term = 8.0;
+    static const double w_scatter[4] = {35.0, 50.0, 77.0, 0.0};  /* + 7 for the recursion combine */
+    const double w_sphere_sample = 14.0;
+
+    double f = w_sample * (double)c->samples + w_pixel * (double)c->pixels;
+    for (int k = 0; k < 8; ++k) f += w_call[k] * (double)c->isect_calls[k] + w_hit[k] * (double)c->isect_hits[k];
+    f += w_root * (double)c->root_checks + w_step * (double)c->sdf_steps;
+    for (int k = 0; k < 128; ++k) f += w_node[k] * (double)c->sdf_nodes[k];
+    f += w_octave * (double)c->noise_octaves;
+    for (int k = 0; k < 4; ++k) f += w_light[k] * (double)c->light_evals[k] + w_scatter[k] * (double)c->scatters[k];
+    f += w_shaded * (double)c->shaded_hits + w_ndl * (double)c->lambert_lights + w_shadow * (double)c->shadow_rays;
+    f += w_term * (double)c->lambert_terms + w_ref_term * (double)c->ref_light_terms;
+    f += w_sphere_sample * (double)c->sphere_samples;
+    return f;
 }

@@ -43,6 +43,38 @@ int rrte_oracle_render(const rrte_scene_ir* scene, const rrte_render_params* par
                        uint8_t* out_rgba8, float* out_f32, uint64_t* shadow_rays,
                        int nthreads, uint32_t row_begin, uint32_t row_end);
 
+/* Instrumented event counts of one render (SURVEY.md §8d "flops per ray = sum over
+ * evaluations of fixed per-op counts tabulated by the oracle").  Filled only by the
+ * counting build (librrte_oracle_count.so, -DRRTE_ORACLE_COUNT); the timed oracle
+ * carries no instrumentation. */
+typedef struct rrte_oracle_counts {
+    uint64_t samples;            /* camera rays generated (pixels * spp)              */
+    uint64_t pixels;             /* pixels finalised (average, gamma, clamp, u8)      */
+    uint64_t isect_calls[8];     /* intersector entries by RRTE_PRIM_* kind           */
+    uint64_t isect_hits[8];      /* hit-attribute computations by kind                */
+    uint64_t root_checks;        /* candidate roots tested (ray_at + range) in cyl/cone/capsule */
+    uint64_t sdf_steps;          /* sphere-tracing steps (one program evaluation each)  */
+    uint64_t sdf_normals;        /* tetrahedral normal estimates (4 evaluations each)  */
+    uint64_t sdf_nodes[128];     /* program node evaluations by op (all evaluations)   */
+    uint64_t noise_octaves;      /* value-noise evaluations (3 per octave per NOISE node) */
+    uint64_t light_evals[4];     /* Light::illuminate by RRTE_LIGHT_* kind            */
+    uint64_t shaded_hits;        /* hits with a material (base colour)                */
+    uint64_t lambert_lights;     /* LAMBERT_SHADOW: N.L evaluations (non-ambient)     */
+    uint64_t shadow_rays;        /* shadow rays built and traced                       */
+    uint64_t lambert_terms;      /* unoccluded diffuse terms added                     */
+    uint64_t ref_light_terms;    /* REFCOMPAT: colour*att terms added                  */
+    uint64_t scatters[4];        /* Material::scatter by RRTE_MAT_* kind               */
+    uint64_t sphere_samples;     /* rand_in_unit_sphere rejection tries                */
+} rrte_oracle_counts;
+
+/* Counting build only: render like rrte_oracle_render and accumulate event counts. */
+int rrte_oracle_render_counted(const rrte_scene_ir* scene, const rrte_render_params* params,
+                               rrte_oracle_counts* counts, int nthreads, uint32_t row_begin, uint32_t row_end);
+
+/* Algorithmic FP32 operations of a count set (weights tabulated in rrte_oracle.c:
+ * add, sub, mul, div, sqrt, min, max and each transcendental = 1; abs/neg/compare = 0). */
+double rrte_oracle_flops(const rrte_oracle_counts* counts);
+
 /* Known-answer-test hooks. */
 int rrte_oracle_intersect(const rrte_scene_ir* scene, uint32_t prim_index,
                           const float origin[3], const float direction[3],
