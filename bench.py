@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stock", action="store_true", help="skip the stock-config secondary measurement")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: gather on the render stream instead of pipelining it against the next frame")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
@@ -153,6 +155,8 @@ def main():
     cfg.band_rows = args.band_rows
     scene = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
+    if world > 1 and not args.no_overlap:
+        prm.flags |= abi.FLAG_GATHER_OVERLAP  # frame k's RCCL gather overlaps frame k+1's render
     ctx = Context(local_rank, jit={"off": abi.JIT_OFF, "on": abi.JIT_ON, "auto": abi.JIT_AUTO}[args.jit])
     lib = ctx.lib
 
@@ -278,6 +282,8 @@ def main():
             "config": {
                 "workload": f"{args.scene} {W}x{H}, {args.mode}, spp=1, pixel-centre jitter"
                             + (f", {args.band_rows}-row bands interleaved over {world} GPUs + RCCL gather to rank 0"
+                               + (" (on the render stream)" if args.no_overlap else
+                                  " pipelined against the next frame's render")
                                if world > 1 else ""),
                 "scene": args.scene, "width": W, "height": H, "mode": args.mode,
                 "primary_rays_per_frame": W * H * prm.samples_per_pixel,

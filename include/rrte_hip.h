@@ -202,6 +202,12 @@ typedef enum rrte_jitter {
 } rrte_jitter;
 
 #define RRTE_FLAG_F32_LINEAR 1u  /* f32 output holds the averaged linear colour (pre-gamma, unclamped) */
+/* rrte_hip_render_gather_async only: pipeline frames.  The gather + de-interleave of
+ * frame k run on the context's comm stream while frame k+1 renders on the caller's
+ * stream (double-buffered slabs, event-ordered); the caller's stream is NOT made to
+ * wait for the gather, so d_full_rgba8 is complete after rrte_hip_synchronize or a
+ * device-wide synchronisation (SURVEY §8e "overlap frame k's gather with k+1's render"). */
+#define RRTE_FLAG_GATHER_OVERLAP 2u
 
 typedef struct rrte_render_params {
     uint32_t width, height;
@@ -294,7 +300,8 @@ rrte_status rrte_hip_comm_init(rrte_ctx* ctx, int nranks, int rank,
 rrte_status rrte_hip_render_gather(rrte_ctx* ctx, const rrte_scene_ir* scene,
                                    const rrte_render_params* params, int root,
                                    uint8_t* out_rgba8);
-/* Async device variant: d_full_rgba8 (root only, W*H*4 bytes) receives the frame. */
+/* Async device variant: d_full_rgba8 (root only, W*H*4 bytes) receives the frame;
+ * all work is ordered on `stream` unless params->flags has RRTE_FLAG_GATHER_OVERLAP. */
 rrte_status rrte_hip_render_gather_async(rrte_ctx* ctx, const rrte_scene_ir* scene,
                                          const rrte_render_params* params, int root,
                                          void* d_full_rgba8, void* stream);

@@ -23,6 +23,7 @@ PERSPECTIVE, ORTHOGRAPHIC = 0, 1
 MODE_REFCOMPAT, MODE_LAMBERT_SHADOW = 0, 1
 JITTER_CENTER, JITTER_RANDOM = 0, 1
 FLAG_F32_LINEAR = 1
+FLAG_GATHER_OVERLAP = 2
 
 SDF_SPHERE, SDF_BOX, SDF_CYLINDER, SDF_PRISM, SDF_TORUS = 1, 2, 3, 4, 5
 SDF_TUBE, SDF_RING, SDF_CONE, SDF_CAPSULE, SDF_ELLIPSOID = 6, 7, 8, 9, 10

@@ -49,6 +49,12 @@ struct rrte_ctx {
     int nranks = 1, rank = 0;
     uint32_t* d_gather = nullptr; size_t cap_gather = 0;
     uint32_t* d_full = nullptr; size_t cap_full = 0;
+    // pipelined gather (RRTE_FLAG_GATHER_OVERLAP): comm stream + two slabs, event-ordered
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_rend[2] = {nullptr, nullptr}, ev_gath[2] = {nullptr, nullptr};
+    uint32_t* d_slab[2] = {nullptr, nullptr};
+    size_t cap_slab[2] = {0, 0};
+    uint64_t gather_frames = 0;
     bool gather_timed = false;
     rrte_stats stats{};
     bool pending_kernel_timing = false;
@@ -596,14 +602,20 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto& kv : c->jit_cache) jit_release(kv.second);
-    void* bufs[] = {c->d_prims, c->d_mats, c->d_lights, c->d_nodes, c->d_bounds, c->d_rgba,
-                    c->d_f32,   c->d_counters, c->d_gather, c->d_full};
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    void* bufs[] = {c->d_prims, c->d_mats,   c->d_lights, c->d_nodes,  c->d_bounds,   c->d_rgba,
+                    c->d_f32,   c->d_counters, c->d_gather, c->d_full, c->d_slab[0], c->d_slab[1]};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
+    for (int i = 0; i < 2; ++i) {
+        if (c->ev_rend[i]) (void)hipEventDestroy(c->ev_rend[i]);
+        if (c->ev_gath[i]) (void)hipEventDestroy(c->ev_gath[i]);
+    }
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -713,6 +725,7 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
     rrte_status r = validate(c, s, p);
     if (r != RRTE_OK) return r;
     if (root < 0 || root >= c->nranks) return fail(c, RRTE_INVALID_ARG, "root %d out of range", root);
+    if (c->rank == root && !d_full) return fail(c, RRTE_INVALID_ARG, "root needs an output buffer");
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
     double up = 0.0;
     if ((r = upload_scene(c, s, st, &up)) != RRTE_OK) return r;
@@ -722,23 +735,55 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
     const uint32_t rows = rows_for_rank(p->height, band, c->nranks, c->rank);
     const uint32_t cap = rows_for_rank(p->height, band, c->nranks, 0);  // rank 0 owns the most rows
     const size_t slice = (size_t)cap * p->width;
-    if (c->nranks == 1) {
-        if (!d_full) return fail(c, RRTE_INVALID_ARG, "null output");
+    // one rank: no exchange (RRTE_FORCE_GATHER=1 still takes the gather path: tests on one GPU)
+    const char* fg = getenv("RRTE_FORCE_GATHER");
+    if (c->nranks == 1 && !(fg && fg[0] == '1' && c->comm)) {
         r = launch(c, s, p, p->height, static_cast<uint32_t*>(d_full), nullptr, st);
         if (r == RRTE_OK) c->pending_primary = (uint64_t)p->width * p->height * p->samples_per_pixel;
         return r;
     }
-    if ((r = ensure(c, c->d_gather, c->cap_gather, slice * (size_t)c->nranks)) != RRTE_OK) return r;
-    uint32_t* mine = c->d_gather + (size_t)c->rank * slice;  // in-place send slot
-    if ((r = launch(c, s, &pp, rows, mine, nullptr, st)) != RRTE_OK) return r;
-    HIPCHK(c, hipEventRecord(c->ev1, st));
-    NCCLCHK(c, ncclGather(mine, c->d_gather, slice * 4, ncclUint8, root, c->comm, st));
-    if (c->rank == root) {
-        if (!d_full) return fail(c, RRTE_INVALID_ARG, "root needs an output buffer");
-        dim3 g((p->width + 255) / 256 < 8 ? (p->width + 255) / 256 : 8, p->height);
-        hipLaunchKernelGGL(deinterleave_kernel, g, dim3(256), 0, st, c->d_gather, static_cast<uint32_t*>(d_full),
-                           p->width, p->height, band, (uint32_t)c->nranks, cap);
-        HIPCHK(c, hipGetLastError());
+    if (!c->comm) return fail(c, RRTE_INVALID_ARG, "rrte_hip_comm_init has not been called");
+    const dim3 dg((p->width + 255) / 256 < 8 ? (p->width + 255) / 256 : 8, p->height);
+    if (!(p->flags & RRTE_FLAG_GATHER_OVERLAP)) {
+        // everything on `st`: render this rank's bands into its slot, gather in place, de-interleave
+        if ((r = ensure(c, c->d_gather, c->cap_gather, slice * (size_t)c->nranks)) != RRTE_OK) return r;
+        uint32_t* mine = c->d_gather + (size_t)c->rank * slice;  // in-place send slot
+        if ((r = launch(c, s, &pp, rows, mine, nullptr, st)) != RRTE_OK) return r;
+        HIPCHK(c, hipEventRecord(c->ev1, st));
+        NCCLCHK(c, ncclGather(mine, c->d_gather, slice * 4, ncclUint8, root, c->comm, st));
+        if (c->rank == root) {
+            hipLaunchKernelGGL(deinterleave_kernel, dg, dim3(256), 0, st, c->d_gather, static_cast<uint32_t*>(d_full),
+                               p->width, p->height, band, (uint32_t)c->nranks, cap);
+            HIPCHK(c, hipGetLastError());
+        }
+    } else {
+        // Pipelined: frame k renders into slab k&1 on `st`; its gather + de-interleave run on the
+        // comm stream once the render's event fires.  The render of frame k+2 (same slab) first
+        // waits for frame k's gather.  Waiting on a never-recorded event is a no-op.
+        if (!c->cstream) {
+            HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+            for (int i = 0; i < 2; ++i) {
+                HIPCHK(c, hipEventCreateWithFlags(&c->ev_rend[i], hipEventDisableTiming));
+                HIPCHK(c, hipEventCreateWithFlags(&c->ev_gath[i], hipEventDisableTiming));
+            }
+        }
+        const int slot = (int)(c->gather_frames & 1u);
+        if (c->cap_slab[slot] < slice * (size_t)c->nranks) HIPCHK(c, hipStreamSynchronize(c->cstream));
+        if ((r = ensure(c, c->d_slab[slot], c->cap_slab[slot], slice * (size_t)c->nranks)) != RRTE_OK) return r;
+        uint32_t* slab = c->d_slab[slot];
+        uint32_t* mine = slab + (size_t)c->rank * slice;
+        HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[slot], 0));
+        if ((r = launch(c, s, &pp, rows, mine, nullptr, st)) != RRTE_OK) return r;
+        HIPCHK(c, hipEventRecord(c->ev_rend[slot], st));
+        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_rend[slot], 0));
+        NCCLCHK(c, ncclGather(mine, slab, slice * 4, ncclUint8, root, c->comm, c->cstream));
+        if (c->rank == root) {
+            hipLaunchKernelGGL(deinterleave_kernel, dg, dim3(256), 0, c->cstream, slab, static_cast<uint32_t*>(d_full),
+                               p->width, p->height, band, (uint32_t)c->nranks, cap);
+            HIPCHK(c, hipGetLastError());
+        }
+        HIPCHK(c, hipEventRecord(c->ev_gath[slot], c->cstream));
+        ++c->gather_frames;
     }
     c->pending_primary = (uint64_t)p->width * rows * p->samples_per_pixel;
     c->stats.upload_ms = up;
@@ -758,8 +803,10 @@ rrte_status rrte_hip_render_gather(rrte_ctx* c, const rrte_scene_ir* s, const rr
         if ((r = ensure(c, c->d_full, c->cap_full, npix)) != RRTE_OK) return r;
         full = c->d_full;
     }
+    rrte_render_params pb = *p;
+    pb.flags &= ~RRTE_FLAG_GATHER_OVERLAP;  // one blocking frame: no pipelining
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    if ((r = rrte_hip_render_gather_async(c, s, p, root, full, c->stream)) != RRTE_OK) return r;
+    if ((r = rrte_hip_render_gather_async(c, s, &pb, root, full, c->stream)) != RRTE_OK) return r;
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     if (c->rank == root && out) HIPCHK(c, hipMemcpyAsync(out, full, npix * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -1,0 +1,79 @@
+"""Multi-GPU frame path on one GPU: a 1-rank RCCL communicator with RRTE_FORCE_GATHER=1 drives
+rrte_hip_render_gather(_async) through the real band render -> ncclGather -> de-interleave
+sequence, in both the single-stream and the pipelined (RRTE_FLAG_GATHER_OVERLAP) form.  Every
+frame must equal the plain single-context render bit for bit.  (N > 1 needs more GPUs than the
+test box has; the band partition itself is covered by tests/test_dist.py with gloo.)"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from rrte_amd import LoweredScene, abi, scenes
+from rrte_amd.math import vec3
+from rrte_amd.renderer import Context
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(n, w=320, h=200):
+    out = []
+    for i in range(n):
+        objs, lights, cam, cfg = scenes.sdf_showcase(w, h)
+        cam.transform.position = vec3(0.0 + 0.7 * i, 8.0 - 0.3 * i, 20.0)
+        cam.look_at((0, 2, 0))
+        out.append((LoweredScene(objs, lights, cam), cfg.lower()))
+    return out
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+def test_gather_path_matches_plain_render(overlap, jit, monkeypatch):
+    import torch
+
+    monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    frames = _frames(5)
+    w, h = frames[0][1].width, frames[0][1].height
+    ref = Context(0, jit=jit)
+    want = []
+    for sc, prm in frames:
+        buf = np.zeros(w * h * 4, dtype=np.uint8)
+        ref.check(ref.lib.rrte_hip_render(ref.h, sc.ref(), C.byref(prm), buf.ctypes.data_as(C.POINTER(C.c_uint8))))
+        want.append(buf)
+    ref.close()
+
+    ctx = Context(0, jit=jit)
+    lib = ctx.lib
+    uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+    ctx.check(lib.rrte_hip_comm_unique_id(uid))
+    ctx.check(lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    outs = [torch.empty(w * h, dtype=torch.int32, device=dev) for _ in frames]
+    for (sc, prm), o in zip(frames, outs):
+        p = abi.RenderParams.from_buffer_copy(prm)
+        if overlap:
+            p.flags |= abi.FLAG_GATHER_OVERLAP
+        ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(p), 0, o.data_ptr(),
+                                                    C.c_void_p(stream.cuda_stream)))
+    ctx.check(lib.rrte_hip_synchronize(ctx.h))
+    for i, o in enumerate(outs):
+        got = o.cpu().numpy().view(np.uint8)
+        assert np.array_equal(got, want[i]), f"frame {i}: {(got != want[i]).sum()} bytes differ"
+    # blocking variant to host memory
+    buf = np.zeros(w * h * 4, dtype=np.uint8)
+    sc, prm = frames[2]
+    ctx.check(lib.rrte_hip_render_gather(ctx.h, sc.ref(), C.byref(prm), 0, buf.ctypes.data_as(C.POINTER(C.c_uint8))))
+    assert np.array_equal(buf, want[2])
+    ctx.close()
+
+
+def test_gather_requires_comm_and_root_buffer(monkeypatch):
+    monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    (sc, prm), = _frames(1, 64, 48)
+    ctx = Context(0)
+    uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+    ctx.check(ctx.lib.rrte_hip_comm_unique_id(uid))
+    ctx.check(ctx.lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
+    assert ctx.lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, None, None) == abi.RRTE_INVALID_ARG
+    assert ctx.lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 1, None, None) == abi.RRTE_INVALID_ARG
+    ctx.close()
