@@ -20,6 +20,11 @@ from pathlib import Path
 
 import numpy as np
 
+# Frames in flight need their streams on distinct hardware queues; HIP's default of 4 per
+# process is shared with torch's and the library's own streams (measured: 4 -> 8 queues takes an
+# N=8 rank's frame from 40 to 24 us at 4 frames in flight).  Must be set before HIP starts.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
@@ -43,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stock", action="store_true", help="skip the stock-config secondary measurement")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="frames in flight: consecutive frames rotate over this many streams + output buffers "
+                         "so one frame's tail overlaps the next frame's start (1 = strictly one after another)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: gather on the render stream instead of pipelining it against the next frame")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
@@ -171,35 +179,44 @@ def main():
         ctx.check(lib.rrte_hip_comm_init(ctx.h, world, rank, idb))
 
     W, H = args.width, args.height
-    full = torch.empty(W * H, dtype=torch.int32, device=dev)
-    # a dedicated (non-null) stream: kernels, events and the gather all go on it
-    stream = torch.cuda.Stream(dev)
+    F = max(1, args.inflight)
+    # dedicated (non-null) streams, one output buffer per frame in flight
+    streams = [torch.cuda.Stream(dev) for _ in range(F)]
+    fulls = [torch.empty(W * H, dtype=torch.int32, device=dev) for _ in range(F)]
+    full, stream = fulls[0], streams[0]
     torch.cuda.set_stream(stream)
-    sptr = C.c_void_p(stream.cuda_stream)
-    assert sptr.value, "need a non-null HIP stream handle"
+    sptrs = [C.c_void_p(s.cuda_stream) for s in streams]
+    assert all(p.value for p in sptrs), "need non-null HIP stream handles"
 
-
-    def step():
+    def step(i=0):
+        j = i % F
         if dist_on:
             ctx.check(lib.rrte_hip_render_gather_async(ctx.h, scene.ref(), C.byref(prm), 0,
-                                                       full.data_ptr() if rank == 0 else None, sptr))
+                                                       fulls[j].data_ptr() if rank == 0 else None, sptrs[j]))
         else:
-            ctx.check(lib.rrte_hip_render_async(ctx.h, scene.ref(), C.byref(prm), full.data_ptr(), None, sptr))
+            ctx.check(lib.rrte_hip_render_async(ctx.h, scene.ref(), C.byref(prm), fulls[j].data_ptr(), None, sptrs[j]))
 
-    for _ in range(max(args.warmup, 2)):  # >= 2: the specialised kernel is compiled on warm-up frames
-        step()
+    for i in range(max(args.warmup, 2)):  # >= 2: the specialised kernel is compiled on warm-up frames
+        step(i)
     torch.cuda.synchronize(dev)
-    ctx.check(lib.rrte_hip_synchronize(ctx.h))  # folds warm-up shadow counts away
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # per-launch kernel duration (roofline): frames strictly one after another on one stream
+    n_seq = min(args.steps, 20)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_seq)]
+    for i in range(n_seq):
+        evs[i][0].record(stream)
+        step(0)
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    launch_ms = [a.elapsed_time(b) for a, b in evs]
+    ctx.check(lib.rrte_hip_synchronize(ctx.h))  # folds warm-up and sequential-pass shadow counts away
+
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        evs[i][0].record(stream)
-        step()
-        evs[i][1].record(stream)
+        step(i)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if dist_on:
@@ -207,7 +224,6 @@ def main():
     ctx.check(lib.rrte_hip_synchronize(ctx.h))
     st = ctx.stats()
     elapsed = t1 - t0
-    launch_ms = [a.elapsed_time(b) for a, b in evs]
     rows = lib.rrte_hip_band_rows_for_rank(H, args.band_rows, world, rank) if dist_on else H
     primary = W * rows * prm.samples_per_pixel * args.steps
     shadow = int(st.shadow_rays)
@@ -243,13 +259,15 @@ def main():
     stock = None
     if world == 1 and not args.no_stock:
         sscene, sprm = stock_config(args)
-        for _ in range(2):
-            ctx.check(lib.rrte_hip_render_async(ctx.h, sscene.ref(), C.byref(sprm), full.data_ptr(), None, sptr))
+        for i in range(2):
+            ctx.check(lib.rrte_hip_render_async(ctx.h, sscene.ref(), C.byref(sprm), fulls[i % F].data_ptr(), None,
+                                                sptrs[i % F]))
         torch.cuda.synchronize(dev)
-        n_stock = 5
+        n_stock = 6
         a = time.perf_counter()
-        for _ in range(n_stock):
-            ctx.check(lib.rrte_hip_render_async(ctx.h, sscene.ref(), C.byref(sprm), full.data_ptr(), None, sptr))
+        for i in range(n_stock):
+            ctx.check(lib.rrte_hip_render_async(ctx.h, sscene.ref(), C.byref(sprm), fulls[i % F].data_ptr(), None,
+                                                sptrs[i % F]))
         torch.cuda.synchronize(dev)
         ts = (time.perf_counter() - a) / n_stock
         stock = {"workload": f"{args.scene} {W}x{H} reference stock config: REFCOMPAT, spp=4, max_depth=50, "
@@ -288,6 +306,7 @@ def main():
                 "scene": args.scene, "width": W, "height": H, "mode": args.mode,
                 "primary_rays_per_frame": W * H * prm.samples_per_pixel,
                 "shadow_rays_per_frame": shadow // args.steps,
+                "frames_in_flight": F,
                 "parallelism": f"rows{world}" if world > 1 else "single",
             },
             "roofline": {
@@ -301,6 +320,7 @@ def main():
                            "rrte::ray_kernel<%s> (generic)" % ("LAMBERT_SHADOW" if args.mode == "lambert_shadow" else "REFCOMPAT")),
                 "jit_compile_ms": round(st.jit_compile_ms, 1) if st.jit_active else None,
                 "avg_launch_ms": round(avg_launch_ms, 5),
+                "avg_launch_note": f"HIP events around {len(launch_ms)} frames run one after another on one stream",
                 "bytes_per_launch": bytes_per_launch,
                 "note": "VALU-bound path (no dense contraction, no MFMA); HBM traffic is the 4 B/pixel frame store",
             },
@@ -319,6 +339,7 @@ def main():
                 "bound": "valu-fp32", "flops_per_frame": flops, "achieved": round(tf, 3), "unit": "TFLOP/s",
                 "peak": VALU_PEAK_TFLOPS, "frac": tf / VALU_PEAK_TFLOPS,
                 "frac_of_unpacked_peak": tf / (VALU_PEAK_TFLOPS / 2),
+                "achieved_at_frame_rate": round(flops / (elapsed / args.steps) / 1e12, 3),
                 "note": "algorithmic FP32 ops from the oracle's instrumented counting build (SURVEY §8d) / "
                         "avg kernel duration; peak = packed-FP32 vector peak (the kernel issues unpacked FP32)"}
             sband = (H // 2 - H // 8, H // 2 + H // 8)  # centre quarter of the frame

@@ -303,18 +303,22 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     if (t > tend) return false;
     const float eps = pr.sdf_hit_eps, scale = pr.sdf_step_scale;
     const uint32_t steps = pr.sdf_max_steps;
+    // One divergent exit per step (hit, or the next t leaves the bound) instead of three: same
+    // t sequence and result as "if (d < eps*t) hit; t += d*scale; if (t > tend) miss" (NaN
+    // included).  (A fully predicated form with a wave-uniform exit was measured slower.)
+    bool hit = false;
 #pragma unroll 1
     for (uint32_t i = 0; i < steps; ++i) {
         f3 p = ray_at(r, t);
         float d = eval(p);
-        if (d < eps * t) {
-            t_hit = t;
-            return true;
-        }
-        t = t + d * scale;
-        if (t > tend) return false;
+        hit = d < eps * t;
+        const float tn = t + d * scale;
+        const bool stop = hit || tn > tend;
+        t = hit ? t : tn;
+        if (stop) break;
     }
-    return false;
+    t_hit = t;
+    return hit;
 }
 
 // Hit attributes of an SDF hit at t: p = Ray::at(t) and the tetrahedral

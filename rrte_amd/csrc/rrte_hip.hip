@@ -51,9 +51,10 @@ struct rrte_ctx {
     uint32_t* d_full = nullptr; size_t cap_full = 0;
     // pipelined gather (RRTE_FLAG_GATHER_OVERLAP): comm stream + two slabs, event-ordered
     hipStream_t cstream = nullptr;
-    hipEvent_t ev_rend[2] = {nullptr, nullptr}, ev_gath[2] = {nullptr, nullptr};
-    uint32_t* d_slab[2] = {nullptr, nullptr};
-    size_t cap_slab[2] = {0, 0};
+    static constexpr int kSlabs = 16;  // frames whose gather may be in flight at once
+    hipEvent_t ev_rend[kSlabs] = {}, ev_gath[kSlabs] = {};
+    uint32_t* d_slab[kSlabs] = {};
+    size_t cap_slab[kSlabs] = {};
     uint64_t gather_frames = 0;
     bool gather_timed = false;
     rrte_stats stats{};
@@ -61,6 +62,13 @@ struct rrte_ctx {
     uint64_t pending_primary = 0;
     // scene-specialised kernels (jit.hip)
     int jit_mode = RRTE_JIT_AUTO;
+    // environment switches, read once at rrte_hip_create (diagnostics / A-B runs / tests)
+    uint32_t env_debug = 0;       // RRTE_DEBUG ablation bits
+    int env_cull = -1;            // RRTE_CULL: -1 unset, 0 off, 1 on
+    bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
+    int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
+    uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
+    struct { uint64_t gen; int mode, jit_mode; bool cull, valid; JitKernel* k; } jit_last{};
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
     std::vector<DPrim> h_prims;                  // host copy of the lowered scene (JIT source)
     std::vector<DMaterial> h_mats;
@@ -349,6 +357,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         return RRTE_OK;
     }
     c->same_scene_renders = 0;
+    ++c->scene_gen;
 
     std::vector<DPrim> prims;
     std::vector<DMaterial> mats;
@@ -425,8 +434,7 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     float m[16];
     mat4_srt(trs, m);
     to_affine12(m, k.cam_xf);
-    const char* dbg = getenv("RRTE_DEBUG");  // ablation bits for profiling only
-    k.debug = dbg ? (uint32_t)strtoul(dbg, nullptr, 0) : 0u;
+    k.debug = c->env_debug;  // RRTE_DEBUG ablation bits (profiling only)
     return k;
 }
 
@@ -444,9 +452,14 @@ uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank
 // so scenes of <= 64 objects; it pays where an occlusion test is expensive (sphere-traced SDF
 // objects) and costs a few percent on all-analytic scenes (measured).  RRTE_CULL=0/1
 // forces it off/on (A/B runs, tests).
-bool cull_policy(const rrte_scene_ir* s, uint32_t mode) {
+int env_cull_setting() {
+    const char* ce = getenv("RRTE_CULL");
+    return ce ? (ce[0] != '0' ? 1 : 0) : -1;
+}
+
+bool cull_policy(const rrte_scene_ir* s, uint32_t mode, int env_cull) {
     if (mode != RRTE_MODE_LAMBERT_SHADOW || s->num_prims > 64) return false;
-    if (const char* ce = getenv("RRTE_CULL")) return ce[0] != '0';
+    if (env_cull >= 0) return env_cull != 0;
     for (uint32_t i = 0; i < s->num_prims; ++i)
         if (s->prims[i].kind == RRTE_PRIM_SDF) return true;
     return false;
@@ -458,16 +471,29 @@ constexpr uint32_t kJitMaxPrims = 128, kJitMaxNodes = 1024;
 
 JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull) {
     if (c->jit_mode == RRTE_JIT_OFF) return nullptr;
+    auto& last = c->jit_last;  // per-frame fast path: same scene, mode and policy as the last frame
+    if (last.valid && last.gen == c->scene_gen && last.mode == mode && last.cull == cull && last.jit_mode == c->jit_mode)
+        return last.k;
     if (c->h_prims.size() > kJitMaxPrims || c->h_nodes.size() > kJitMaxNodes) return nullptr;
     std::string key(c->scene_key.begin(), c->scene_key.end());
     key.push_back((char)mode);
     key.push_back((char)cull);
+    auto remember = [&](JitKernel* k) {
+        last.gen = c->scene_gen;
+        last.mode = mode;
+        last.jit_mode = c->jit_mode;
+        last.cull = cull;
+        last.k = k;
+        last.valid = true;
+        return k;
+    };
     auto it = c->jit_cache.find(key);
-    if (it != c->jit_cache.end()) return it->second.fn ? &it->second : nullptr;
+    if (it != c->jit_cache.end()) return remember(it->second.fn ? &it->second : nullptr);
     if (!(c->jit_mode == RRTE_JIT_ON || c->same_scene_renders >= 1)) return nullptr;
     if (c->jit_cache.size() >= 32) {
         for (auto& kv : c->jit_cache) jit_release(kv.second);
         c->jit_cache.clear();
+        last.valid = false;
     }
     std::string src = jit_source(c->h_prims.data(), (uint32_t)c->h_prims.size(), c->h_mats.data(),
                                  (uint32_t)c->h_mats.size(), c->h_lights.data(), (uint32_t)c->h_lights.size(),
@@ -482,14 +508,14 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull) {
     }
     auto& slot = c->jit_cache[key];
     slot = jk;
-    return slot.fn ? &slot : nullptr;
+    return remember(slot.fn ? &slot : nullptr);
 }
 
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
                    uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     KParams k = make_params(c, s, p, rows);
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, s->num_prims, s->num_lights, s->num_materials};
-    const bool cull = cull_policy(s, p->mode);
+    const bool cull = cull_policy(s, p->mode, c->env_cull);
     Cull cl{cull ? c->d_bounds : nullptr, s->num_prims};
     dim3 grid((p->width + 15) / 16, (rows + 15) / 16), block(256);
     if (rows == 0) return RRTE_OK;
@@ -577,6 +603,16 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (!c) return RRTE_HIP_ERROR;
     c->device = device;
     if (const char* j = getenv("RRTE_JIT")) c->jit_mode = (int)strtol(j, nullptr, 0);
+    if (const char* d = getenv("RRTE_DEBUG")) c->env_debug = (uint32_t)strtoul(d, nullptr, 0);
+    c->env_cull = env_cull_setting();
+    if (const char* g = getenv("RRTE_FORCE_GATHER")) c->env_force_gather = g[0] == '1';
+    if (const char* e = getenv("RRTE_EMULATE_RANK")) {
+        int n = 0, r = 0;
+        if (sscanf(e, "%d:%d", &n, &r) == 2 && n > 1 && r >= 0 && r < n) {
+            c->emu_nranks = n;
+            c->emu_rank = r;
+        }
+    }
     auto bail = [&](hipError_t e) {
         (void)e;
         rrte_hip_destroy(c);
@@ -603,15 +639,17 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto& kv : c->jit_cache) jit_release(kv.second);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
-    void* bufs[] = {c->d_prims, c->d_mats,   c->d_lights, c->d_nodes,  c->d_bounds,   c->d_rgba,
-                    c->d_f32,   c->d_counters, c->d_gather, c->d_full, c->d_slab[0], c->d_slab[1]};
+    void* bufs[] = {c->d_prims, c->d_mats,   c->d_lights, c->d_nodes,  c->d_bounds,
+                    c->d_rgba,  c->d_f32,    c->d_counters, c->d_gather, c->d_full};
     for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    for (uint32_t* b : c->d_slab)
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < rrte_ctx::kSlabs; ++i) {
         if (c->ev_rend[i]) (void)hipEventDestroy(c->ev_rend[i]);
         if (c->ev_gath[i]) (void)hipEventDestroy(c->ev_gath[i]);
     }
@@ -643,13 +681,22 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
     double up = 0.0;
     if ((r = upload_scene(c, s, st, &up)) != RRTE_OK) return r;
     const int nr = c->nranks, rk = c->rank;
-    c->nranks = 1;
-    c->rank = 0;
-    r = launch(c, s, p, p->height, static_cast<uint32_t*>(d_rgba), static_cast<float4*>(d_f32), st);
+    uint32_t rows = p->height;
+    rrte_render_params pe = *p;
+    if (c->emu_nranks > 1) {  // diagnostic: exactly one rank's share of a multi-GPU frame, packed
+        c->nranks = c->emu_nranks;
+        c->rank = c->emu_rank;
+        pe.band_rows = p->band_rows ? p->band_rows : 16;
+        rows = rows_for_rank(p->height, pe.band_rows, c->nranks, c->rank);
+    } else {
+        c->nranks = 1;
+        c->rank = 0;
+    }
+    r = launch(c, s, &pe, rows, static_cast<uint32_t*>(d_rgba), static_cast<float4*>(d_f32), st);
     c->nranks = nr;
     c->rank = rk;
     if (r != RRTE_OK) return r;
-    c->pending_primary = (uint64_t)p->width * p->height * p->samples_per_pixel;
+    c->pending_primary = (uint64_t)p->width * rows * p->samples_per_pixel;
     c->stats.upload_ms = up;
     c->stats.frames++;
     return RRTE_OK;
@@ -682,7 +729,7 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
     lower_scene(s, prims, mats, lights);
     std::string src = jit_source(prims.data(), (uint32_t)prims.size(), mats.data(), (uint32_t)mats.size(),
                                  lights.data(), (uint32_t)lights.size(), s->sdf_nodes, s->num_sdf_nodes, mode,
-                                 cull_policy(s, (uint32_t)mode));
+                                 cull_policy(s, (uint32_t)mode, env_cull_setting()));
     std::string msg;
     bool ok = jit_compile_only(src, msg);
     if (log && log_len) {
@@ -736,8 +783,7 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
     const uint32_t cap = rows_for_rank(p->height, band, c->nranks, 0);  // rank 0 owns the most rows
     const size_t slice = (size_t)cap * p->width;
     // one rank: no exchange (RRTE_FORCE_GATHER=1 still takes the gather path: tests on one GPU)
-    const char* fg = getenv("RRTE_FORCE_GATHER");
-    if (c->nranks == 1 && !(fg && fg[0] == '1' && c->comm)) {
+    if (c->nranks == 1 && !(c->env_force_gather && c->comm)) {
         r = launch(c, s, p, p->height, static_cast<uint32_t*>(d_full), nullptr, st);
         if (r == RRTE_OK) c->pending_primary = (uint64_t)p->width * p->height * p->samples_per_pixel;
         return r;
@@ -757,17 +803,18 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
             HIPCHK(c, hipGetLastError());
         }
     } else {
-        // Pipelined: frame k renders into slab k&1 on `st`; its gather + de-interleave run on the
-        // comm stream once the render's event fires.  The render of frame k+2 (same slab) first
-        // waits for frame k's gather.  Waiting on a never-recorded event is a no-op.
+        // Pipelined: frame k renders into slab k % kSlabs on `st` (frames may come on different
+        // streams and overlap); its gather + de-interleave run on the comm stream, in frame order,
+        // once the render's event fires.  The render of frame k + kSlabs (same slab) first waits
+        // for frame k's gather.  Waiting on a never-recorded event is a no-op.
         if (!c->cstream) {
             HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < rrte_ctx::kSlabs; ++i) {
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_rend[i], hipEventDisableTiming));
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_gath[i], hipEventDisableTiming));
             }
         }
-        const int slot = (int)(c->gather_frames & 1u);
+        const int slot = (int)(c->gather_frames % rrte_ctx::kSlabs);
         if (c->cap_slab[slot] < slice * (size_t)c->nranks) HIPCHK(c, hipStreamSynchronize(c->cstream));
         if ((r = ensure(c, c->d_slab[slot], c->cap_slab[slot], slice * (size_t)c->nranks)) != RRTE_OK) return r;
         uint32_t* slab = c->d_slab[slot];
