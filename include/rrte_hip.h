@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RRTE_ABI_VERSION 1u
+#define RRTE_ABI_VERSION 2u
 
 /* ------------------------------------------------------------------ status */
 typedef enum rrte_status {
@@ -59,8 +59,18 @@ typedef enum rrte_prim_kind {
     RRTE_PRIM_CYLINDER = 4, /* primitives.rs:419-465 p: center[0..2], radius[3], height[4] */
     RRTE_PRIM_CONE = 5,     /* primitives.rs:520-571 p: center[0..2], radius[3], height[4] */
     RRTE_PRIM_CAPSULE = 6,  /* primitives.rs:626-725 p: center[0..2], radius[3], height[4] */
-    RRTE_PRIM_SDF = 7       /* build-defined SDFObject: sphere-traced node program;
+    RRTE_PRIM_SDF = 7,      /* build-defined SDFObject: sphere-traced node program;
                                p: bounding sphere center[0..2], radius[3]                 */
+    RRTE_PRIM_MESH = 8      /* triangle mesh (rrte-assets MeshAsset, asset.rs:53-65): triangles
+                               sdf_first .. sdf_first+sdf_count-1 of rrte_scene_ir.mesh_indices
+                               (3 vertex indices each).  Every triangle is Triangle::intersect
+                               (primitives.rs:208-244) with set_normals(n0,n1,n2) -- the vertex
+                               normals, already normalised by the caller -- and the mesh is the
+                               closest hit over its triangles in index order (strict '<': the
+                               lower index wins a tie), i.e. exactly a Vec<Triangle> in the
+                               object list.  Like Triangle it ignores trs (bake the entity
+                               transform into the vertices).  The device traverses a BVH built
+                               once per scene; see DESIGN.md §5.                          */
 } rrte_prim_kind;
 
 /* One SceneObject lowered to POD (192 bytes).  trs is the object's
@@ -225,12 +235,26 @@ typedef struct rrte_render_params {
 } rrte_render_params;           /* 64 bytes */
 
 /* ---------------------------------------------------------------- scene IR */
+/* MeshAsset::Vertex (asset.rs:60-65) position + normal; uv and colour do not
+ * enter the ray loop. */
+typedef struct rrte_mesh_vertex {
+    float position[3];
+    float normal[3];
+} rrte_mesh_vertex;        /* 24 bytes */
+
 typedef struct rrte_scene_ir {
     const rrte_prim* prims;         uint32_t num_prims;
     const rrte_material* materials; uint32_t num_materials;
     const rrte_light* lights;       uint32_t num_lights;
     const rrte_sdf_node* sdf_nodes; uint32_t num_sdf_nodes;
     rrte_camera camera;
+    /* triangle meshes (RRTE_PRIM_MESH): shared vertex pool, 3 indices per triangle */
+    const rrte_mesh_vertex* mesh_vertices; uint32_t num_mesh_vertices;
+    const uint32_t* mesh_indices;          uint32_t num_mesh_indices;
+    /* Mesh data version (the analogue of Scene::is_dirty, crates/rrte-scene/src/lib.rs:310-312):
+     * nonzero = caller-maintained stamp, the device copy and BVH are rebuilt when the stamp,
+     * the array addresses or the counts change; 0 = compare the mesh arrays byte by byte. */
+    uint64_t mesh_version;
 } rrte_scene_ir;
 
 typedef struct rrte_stats {

@@ -90,8 +90,9 @@ def render(scene, params, nthreads=None, rows=None, want_f32=True, linear=False)
 
 class Counts(C.Structure):
     """Mirror of rrte_oracle_counts (rrte_oracle.h)."""
-    _fields_ = [("samples", C.c_uint64), ("pixels", C.c_uint64), ("isect_calls", C.c_uint64 * 8),
-                ("isect_hits", C.c_uint64 * 8), ("root_checks", C.c_uint64), ("sdf_steps", C.c_uint64),
+    _fields_ = [("samples", C.c_uint64), ("pixels", C.c_uint64), ("isect_calls", C.c_uint64 * 16),
+                ("isect_hits", C.c_uint64 * 16), ("mesh_tri_tests", C.c_uint64), ("root_checks", C.c_uint64),
+                ("sdf_steps", C.c_uint64),
                 ("sdf_normals", C.c_uint64), ("sdf_nodes", C.c_uint64 * 128), ("noise_octaves", C.c_uint64),
                 ("light_evals", C.c_uint64 * 4), ("shaded_hits", C.c_uint64), ("lambert_lights", C.c_uint64),
                 ("shadow_rays", C.c_uint64), ("lambert_terms", C.c_uint64), ("ref_light_terms", C.c_uint64),

@@ -507,9 +507,38 @@ static inline void local_ray(const rrte_prim* pr, const ray* r, ray* lr, float m
     *lr = ray_new(m4_point(inv, r->o), vnorm(m4_vector(inv, r->d)));
 }
 
+/* Triangle::intersect (primitives.rs:208-244), Moller-Trumbore: the test part.  On success
+ * out->t, out->p and the barycentrics (u, v in out->n.x, out->n.y) are set. */
+static int tri_intersect(v3 v0, v3 v1, v3 v2, const ray* r, float t_min, float t_max, hit* out) {
+    v3 e1 = vsub(v1, v0), e2 = vsub(v2, v0);
+    v3 h = vcross(r->d, e2);
+    float a = vdot(e1, h);
+    if (a > -1e-6f && a < 1e-6f) return 0;
+    float f = 1.0f / a;
+    v3 s = vsub(r->o, v0);
+    float u = f * vdot(s, h);
+    if (u < 0.0f || u > 1.0f) return 0;
+    v3 q = vcross(s, e1);
+    float v = f * vdot(r->d, q);
+    if (v < 0.0f || u + v > 1.0f) return 0;
+    float t = f * vdot(e2, q);
+    if (t < t_min || t > t_max) return 0;
+    out->t = t;
+    out->p = ray_at(r, t);
+    out->n = V(u, v, 0.0f);
+    return 1;
+}
+/* ... and the attribute part: barycentric normal (primitives.rs:240-243), HitInfo::new. */
+static void tri_attributes(v3 n0, v3 n1, v3 n2, const ray* r, hit* io) {
+    float u = io->n.x, v = io->n.y;
+    float w = 1.0f - u - v;
+    v3 n = vnorm(vadd(vadd(vmuls(n0, w), vmuls(n1, u)), vmuls(n2, v)));
+    *io = hit_new(io->t, io->p, n, r);
+}
+
 /* SceneObject::intersect dispatch (primitives.rs:57-725). */
 static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_min, float t_max, hit* out) {
-    CNT(isect_calls[pr->kind & 7u]);
+    CNT(isect_calls[pr->kind & 15u]);
     switch (pr->kind) {
     case RRTE_PRIM_SPHERE: { /* primitives.rs:57-81 */
         v3 ctr = vload(pr->p);
@@ -542,27 +571,28 @@ static int intersect(const octx* c, const rrte_prim* pr, const ray* r, float t_m
         *out = hit_new(t, p, denom < 0.0f ? n : vneg(n), r);
         return 1;
     }
-    case RRTE_PRIM_TRIANGLE: { /* primitives.rs:208-244 (Moller-Trumbore) */
-        v3 v0 = vload(pr->p), v1 = vload(pr->p + 3), v2 = vload(pr->p + 6);
-        v3 e1 = vsub(v1, v0), e2 = vsub(v2, v0);
-        v3 h = vcross(r->d, e2);
-        float a = vdot(e1, h);
-        if (a > -1e-6f && a < 1e-6f) return 0;
-        float f = 1.0f / a;
-        v3 s = vsub(r->o, v0);
-        float u = f * vdot(s, h);
-        if (u < 0.0f || u > 1.0f) return 0;
-        v3 q = vcross(s, e1);
-        float v = f * vdot(r->d, q);
-        if (v < 0.0f || u + v > 1.0f) return 0;
-        float t = f * vdot(e2, q);
-        if (t < t_min || t > t_max) return 0;
-        v3 p = ray_at(r, t);
-        float w = 1.0f - u - v;
-        v3 n0 = vload(pr->p + 9), n1 = vload(pr->p + 12), n2 = vload(pr->p + 15);
-        v3 n = vnorm(vadd(vadd(vmuls(n0, w), vmuls(n1, u)), vmuls(n2, v)));
-        CNT(isect_hits[pr->kind & 7u]);
-        *out = hit_new(t, p, n, r);
+    case RRTE_PRIM_TRIANGLE: /* primitives.rs:208-244 (Moller-Trumbore) */
+        if (!tri_intersect(vload(pr->p), vload(pr->p + 3), vload(pr->p + 6), r, t_min, t_max, out)) return 0;
+        CNT(isect_hits[pr->kind & 15u]);
+        tri_attributes(vload(pr->p + 9), vload(pr->p + 12), vload(pr->p + 15), r, out);
+        return 1;
+    case RRTE_PRIM_MESH: { /* a Vec<Triangle> with set_normals: closest over triangles, strict '<' */
+        const rrte_mesh_vertex* vx = c->s->mesh_vertices;
+        const uint32_t* ix = c->s->mesh_indices + (size_t)pr->sdf_first * 3;
+        int found = 0, win = 0;
+        hit best = {0}, h = {0};
+        for (uint32_t k = 0; k < pr->sdf_count; ++k) {
+            CNT(mesh_tri_tests);
+            const rrte_mesh_vertex *a = &vx[ix[3 * k]], *b = &vx[ix[3 * k + 1]], *cc = &vx[ix[3 * k + 2]];
+            if (tri_intersect(vload(a->position), vload(b->position), vload(cc->position), r, t_min, t_max, &h)) {
+                if (!found || h.t < best.t) { best = h; win = (int)k; found = 1; }
+            }
+        }
+        if (!found) return 0;
+        CNT(isect_hits[RRTE_PRIM_MESH]);
+        const rrte_mesh_vertex *a = &vx[ix[3 * win]], *b = &vx[ix[3 * win + 1]], *cc = &vx[ix[3 * win + 2]];
+        tri_attributes(vload(a->normal), vload(b->normal), vload(cc->normal), r, &best);
+        *out = best;
         return 1;
     }
     case RRTE_PRIM_CUBE: { /* primitives.rs:301-364 */
@@ -1031,7 +1061,13 @@ static int validate_scene(const rrte_scene_ir* s, const rrte_render_params* p) {
     if (s->num_materials && !s->materials) return 0;
     for (uint32_t i = 0; i < s->num_prims; ++i) {
         const rrte_prim* pr = &s->prims[i];
-        if (pr->kind > RRTE_PRIM_SDF) return 0;
+        if (pr->kind > RRTE_PRIM_MESH) return 0;
+        if (pr->kind == RRTE_PRIM_MESH) {
+            if ((uint64_t)(pr->sdf_first + (uint64_t)pr->sdf_count) * 3 > s->num_mesh_indices) return 0;
+            if (pr->sdf_count && (!s->mesh_indices || !s->mesh_vertices)) return 0;
+            for (uint64_t k = (uint64_t)pr->sdf_first * 3; k < (uint64_t)(pr->sdf_first + (uint64_t)pr->sdf_count) * 3; ++k)
+                if (s->mesh_indices[k] >= s->num_mesh_vertices) return 0;
+        }
         if (pr->kind == RRTE_PRIM_SDF) {
             if (!s->sdf_nodes || (uint64_t)pr->sdf_first + pr->sdf_count > s->num_sdf_nodes) return 0;
             if (!sdf_validate(s->sdf_nodes + pr->sdf_first, pr->sdf_count)) return 0;
@@ -1130,9 +1166,10 @@ double rrte_oracle_flops(const rrte_oracle_counts* c) {
     /* u,v (4) + generate_ray: ndc 4, tan/half 3, scale 2, normalize 10, quat*vec 38, Ray::new 10 (67) + accumulate 4 */
     const double w_sample = 75.0;
     const double w_pixel = 11.0;                      /* /spp 4, powf x3, *255 x4 */
-    /*                              sphere plane tri  cube cyl  cone caps  sdf(bound test) */
-    static const double w_call[8] = {23.0, 14.0, 30.0, 146.0, 79.0, 91.0, 133.0, 21.0};
-    static const double w_hit[8] = {22.0, 11.0, 60.0, 54.0, 52.0, 64.0, 60.0, 36.0};
+    /*                              sphere plane tri  cube cyl  cone caps  sdf(bound test)  mesh */
+    static const double w_call[16] = {23.0, 14.0, 30.0, 146.0, 79.0, 91.0, 133.0, 21.0, 0.0};
+    static const double w_hit[16] = {22.0, 11.0, 60.0, 54.0, 52.0, 64.0, 60.0, 36.0, 60.0};
+    const double w_tri_test = 30.0;                   /* Moller-Trumbore to its usual early exit */
     const double w_root = 7.0, w_step = 9.0;
     double w_node[128] = {0};
     w_node[RRTE_SDF_SPHERE] = 10; w_node[RRTE_SDF_BOX] = 22; w_node[RRTE_SDF_CYLINDER] = 19;
@@ -1151,7 +1188,8 @@ double rrte_oracle_flops(const rrte_oracle_counts* c) {
     const double w_sphere_sample = 14.0;
 
     double f = w_sample * (double)c->samples + w_pixel * (double)c->pixels;
-    for (int k = 0; k < 8; ++k) f += w_call[k] * (double)c->isect_calls[k] + w_hit[k] * (double)c->isect_hits[k];
+    for (int k = 0; k < 16; ++k) f += w_call[k] * (double)c->isect_calls[k] + w_hit[k] * (double)c->isect_hits[k];
+    f += w_tri_test * (double)c->mesh_tri_tests;
     f += w_root * (double)c->root_checks + w_step * (double)c->sdf_steps;
     for (int k = 0; k < 128; ++k) f += w_node[k] * (double)c->sdf_nodes[k];
     f += w_octave * (double)c->noise_octaves;

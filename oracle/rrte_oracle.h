@@ -50,8 +50,9 @@ int rrte_oracle_render(const rrte_scene_ir* scene, const rrte_render_params* par
 typedef struct rrte_oracle_counts {
     uint64_t samples;            /* camera rays generated (pixels * spp)              */
     uint64_t pixels;             /* pixels finalised (average, gamma, clamp, u8)      */
-    uint64_t isect_calls[8];     /* intersector entries by RRTE_PRIM_* kind           */
-    uint64_t isect_hits[8];      /* hit-attribute computations by kind                */
+    uint64_t isect_calls[16];    /* intersector entries by RRTE_PRIM_* kind           */
+    uint64_t isect_hits[16];     /* hit-attribute computations by kind                */
+    uint64_t mesh_tri_tests;     /* Moller-Trumbore tests inside meshes (linear scan)   */
     uint64_t root_checks;        /* candidate roots tested (ray_at + range) in cyl/cone/capsule */
     uint64_t sdf_steps;          /* sphere-tracing steps (one program evaluation each)  */
     uint64_t sdf_normals;        /* tetrahedral normal estimates (4 evaluations each)  */

@@ -13,4 +13,6 @@ from .renderer import (AmbientLight, BendDeformer, Camera, Capsule, ChainDeforme
                        SDFSphere, SDFTorus, SDFTube, Sphere, SpotLight, TaperDeformer, Triangle,
                        TwistDeformer, WaveDeformer)
 
+from .mesh import Mesh, load_scene_asset  # noqa: F401,E402
+
 __version__ = "0.1.0"

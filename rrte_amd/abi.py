@@ -16,12 +16,13 @@ LIB_PATH = Path(os.environ.get("RRTE_HIP_LIB", _HERE / "lib" / "librrte_hip.so")
 RRTE_OK, RRTE_INVALID_ARG, RRTE_HIP_ERROR, RRTE_RCCL_ERROR, RRTE_UNSUPPORTED_PRIM, RRTE_NO_DEVICE = range(6)
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "HIP_ERROR", 3: "RCCL_ERROR", 4: "UNSUPPORTED_PRIM", 5: "NO_DEVICE"}
 
-PRIM_SPHERE, PRIM_PLANE, PRIM_TRIANGLE, PRIM_CUBE, PRIM_CYLINDER, PRIM_CONE, PRIM_CAPSULE, PRIM_SDF = range(8)
+PRIM_SPHERE, PRIM_PLANE, PRIM_TRIANGLE, PRIM_CUBE, PRIM_CYLINDER, PRIM_CONE, PRIM_CAPSULE, PRIM_SDF, PRIM_MESH = range(9)
 MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_EMISSIVE = range(4)
 LIGHT_POINT, LIGHT_DIRECTIONAL, LIGHT_SPOT, LIGHT_AMBIENT = range(4)
 PERSPECTIVE, ORTHOGRAPHIC = 0, 1
 MODE_REFCOMPAT, MODE_LAMBERT_SHADOW = 0, 1
 JITTER_CENTER, JITTER_RANDOM = 0, 1
+ABI_VERSION = 2  # include/rrte_hip.h RRTE_ABI_VERSION
 FLAG_F32_LINEAR = 1
 FLAG_GATHER_OVERLAP = 2
 
@@ -80,6 +81,10 @@ class RenderParams(C.Structure):
     ]
 
 
+class MeshVertex(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("normal", C.c_float * 3)]
+
+
 class SceneIR(C.Structure):
     _fields_ = [
         ("prims", C.POINTER(Prim)), ("num_prims", C.c_uint32),
@@ -87,6 +92,9 @@ class SceneIR(C.Structure):
         ("lights", C.POINTER(Light)), ("num_lights", C.c_uint32),
         ("sdf_nodes", C.POINTER(SdfNode)), ("num_sdf_nodes", C.c_uint32),
         ("camera", Camera),
+        ("mesh_vertices", C.POINTER(MeshVertex)), ("num_mesh_vertices", C.c_uint32),
+        ("mesh_indices", C.POINTER(C.c_uint32)), ("num_mesh_indices", C.c_uint32),
+        ("mesh_version", C.c_uint64),
     ]
 
 
@@ -144,7 +152,7 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rrte_hip_abi_version() != 1:
+    if lib.rrte_hip_abi_version() != ABI_VERSION:
         raise RuntimeError("librrte_hip.so ABI version mismatch")
     _lib = lib
     return lib

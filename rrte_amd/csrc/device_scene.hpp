@@ -111,7 +111,11 @@ struct Ray { f3 o, d; };
 __device__ __forceinline__ Ray ray_new(f3 o, f3 d) { return Ray{o, vnorm(d)}; }
 __device__ __forceinline__ f3 ray_at(const Ray& r, float t) { return vadd(r.o, vmuls(r.d, t)); }
 
-struct Hit { float t; f3 p, n; bool front; };
+__device__ __forceinline__ bool finite3(f3 a) {
+    return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
+}
+
+struct Hit { float t; f3 p, n; bool front; uint32_t sub; };  // sub: mesh triangle slot of the hit
 // HitInfo::new (ray.rs:45-56)
 __device__ __forceinline__ void hit_new(Hit& h, float t, f3 p, f3 outward, const Ray& r) {
     h.t = t;

@@ -21,6 +21,19 @@ constexpr uint32_t kCounterStride = 16;   // u64 per shard: one 128-B line each
 // members are static constexpr arrays and counts: the same device code below
 // then fully unrolls its object / node / light loops and folds every scene
 // constant into the instruction stream.
+// Triangle-mesh data (RRTE_PRIM_MESH), built once per scene on the host (rrte_hip.hip,
+// build_mesh_bvh).  BVH node k = nodes[2k] (box min xyz, w = first child / first triangle slot)
+// and nodes[2k+1] (box max xyz, w = bit 31 set: interior, split axis in bits 0-1, children a and
+// a+1; else leaf triangle count).  Triangle slot k = tris[3k..3k+2]: v0 (w = the triangle's
+// index within its mesh), e1 = v1-v0, e2 = v2-v0; norms[3k..3k+2] = vertex normals.  perm maps
+// (mesh's first slot + original index) -> slot, for the original-order scan.
+struct MeshView {
+    const float4* __restrict__ nodes;
+    const float4* __restrict__ tris;
+    const float4* __restrict__ norms;
+    const uint32_t* __restrict__ perm;
+};
+
 struct SceneView {
     static constexpr bool kStatic = false;
     const DPrim* __restrict__ prims;
@@ -28,6 +41,7 @@ struct SceneView {
     const DLight* __restrict__ lights;
     const rrte_sdf_node* __restrict__ nodes;
     uint32_t num_prims, num_lights, num_materials;
+    MeshView mesh;
 };
 
 // Loop over objects / lights: a plain loop for the runtime scene, compile-time
@@ -574,9 +588,131 @@ __device__ __forceinline__ bool isect_sdf(const DPrim& pr, const EVAL& eval, con
     return true;
 }
 
+// ---------------------------------------------------------------- meshes
+// Moller-Trumbore exactly as Triangle::intersect (primitives.rs:208-244), with e1 = v1-v0 and
+// e2 = v2-v0 precomputed on the host (the same f32 subtractions).
+__device__ __forceinline__ bool mt_test(f3 v0, f3 e1, f3 e2, const Ray& r, float t_min, float t_max, float& t,
+                                        float& u, float& v) {
+    f3 h = vcross(r.d, e2);
+    float a = vdot(e1, h);
+    if (a > -1e-6f && a < 1e-6f) return false;
+    float f = 1.0f / a;
+    f3 s = vsub(r.o, v0);
+    u = f * vdot(s, h);
+    if (u < 0.0f || u > 1.0f) return false;
+    f3 q = vcross(s, e1);
+    v = f * vdot(r.d, q);
+    if (v < 0.0f || u + v > 1.0f) return false;
+    t = f * vdot(e2, q);
+    if (t < t_min || t > t_max) return false;
+    return true;
+}
+
+__device__ __forceinline__ f3 xyz(float4 a) { return V(a.x, a.y, a.z); }
+
+// Hit attributes of triangle slot k: re-run the test for (u, v), barycentric normal
+// (primitives.rs:240-243), HitInfo::new.
+__device__ __forceinline__ bool mesh_tri_hit(const MeshView& mv, uint32_t k, const Ray& r, float t_min, float t_max,
+                                             Hit& out) {
+    float t, u, v;
+    if (!mt_test(xyz(mv.tris[3 * k]), xyz(mv.tris[3 * k + 1]), xyz(mv.tris[3 * k + 2]), r, t_min, t_max, t, u, v))
+        return false;
+    f3 p = ray_at(r, t);
+    float w = 1.0f - u - v;
+    f3 n = vnorm(vadd(vadd(vmuls(xyz(mv.norms[3 * k]), w), vmuls(xyz(mv.norms[3 * k + 1]), u)),
+                      vmuls(xyz(mv.norms[3 * k + 2]), v)));
+    hit_new(out, t, p, n, r);
+    out.sub = k;
+    return true;
+}
+
+constexpr int kMeshStack = 32;  // BVH depth is capped below this at build time
+__device__ __forceinline__ uint32_t* mesh_stack() {
+    __shared__ uint32_t stk[kMeshStack * 256];  // [depth][lane of the 256-thread workgroup]
+    return stk + threadIdx.x;
+}
+
+// Slab test against an (inflated) node box, clipped to [t_min, t_max]: the entry t, or +inf.
+__device__ __forceinline__ float box_entry(float4 lo, float4 hi, f3 o, f3 inv, float t_min, float t_max) {
+    float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
+    float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
+    float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
+    float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), t_min));
+    float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), t_max));
+    return tn <= tf ? tn : kInf;
+}
+
+// The mesh as a Vec<Triangle>: closest hit over its triangles in index order (strict '<', the
+// lower index wins a tie) or, with ANY, whether any triangle is hit.  The BVH visits the near
+// child first and prunes boxes entered beyond the current best; boxes are inflated at build time
+// so the pruning never drops a triangle the test would accept (meshes).  Rays with
+// a non-finite component take the original-order scan (every test then "hits" with t = NaN, as
+// in the reference, and the lowest index wins).  Writes t and the triangle slot (out.sub).
+template <bool ANY>
+__device__ __forceinline__ bool isect_mesh(const DPrim& pr, const MeshView& mv, const Ray& r, float t_min,
+                                           float t_max, Hit& out) {
+    const uint32_t count = pr.sdf_count, base = (uint32_t)pr.p[0];
+    bool found = false;
+    float best = kInf;
+    uint32_t best_k = 0u, best_orig = 0u;
+    if (!(finite3(r.o) && finite3(r.d))) {
+        for (uint32_t i = 0; i < count; ++i) {
+            const uint32_t k = mv.perm[base + i];
+            float t, u, v;
+            if (mt_test(xyz(mv.tris[3 * k]), xyz(mv.tris[3 * k + 1]), xyz(mv.tris[3 * k + 2]), r, t_min, t_max, t, u, v)) {
+                if (!found || t < best) {
+                    best = t;
+                    best_k = k;
+                    found = true;
+                    if (ANY) break;
+                }
+            }
+        }
+    } else {
+        const f3 inv = V(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+        uint32_t* stk = mesh_stack();
+        int sp = 0;
+        uint32_t node = pr.sdf_first;
+        for (;;) {
+            const float4 lo = mv.nodes[2 * node], hi = mv.nodes[2 * node + 1];
+            if (box_entry(lo, hi, r.o, inv, t_min, found ? fminf(best, t_max) : t_max) != kInf) {
+                const uint32_t meta = __float_as_uint(hi.w), a = __float_as_uint(lo.w);
+                if (meta & 0x80000000u) {  // interior: near child first (sign of d on the split axis)
+                    const uint32_t axis = meta & 3u;
+                    const float da = axis == 0u ? r.d.x : (axis == 1u ? r.d.y : r.d.z);
+                    const bool lfirst = !(da < 0.0f);
+                    stk[(sp++) * 256] = lfirst ? a + 1u : a;
+                    node = lfirst ? a : a + 1u;
+                    continue;
+                }
+                for (uint32_t k = a; k < a + meta; ++k) {
+                    const float4 A = mv.tris[3 * k];
+                    float t, u, v;
+                    if (mt_test(xyz(A), xyz(mv.tris[3 * k + 1]), xyz(mv.tris[3 * k + 2]), r, t_min, t_max, t, u, v)) {
+                        const uint32_t orig = __float_as_uint(A.w);
+                        if (!found || t < best || (t == best && orig < best_orig)) {
+                            best = t;
+                            best_k = k;
+                            best_orig = orig;
+                            found = true;
+                        }
+                        if (ANY) break;
+                    }
+                }
+                if (ANY && found) break;
+            }
+            if (sp == 0) break;
+            node = stk[(--sp) * 256];
+        }
+    }
+    out.t = best;
+    out.sub = best_k;
+    return found;
+}
+
 // SceneObject::intersect dispatch, runtime object index: switch on the kind
 // (wave-uniform -> scalar branches).
-template <bool NEED_HIT, class S>
+template <bool NEED_HIT, class S, bool ANY = false>
 __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t_max,
                                              Hit& out) {
     const DPrim& pr = sc.prims[i];
@@ -590,13 +726,14 @@ __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray&
     case RRTE_PRIM_CAPSULE: return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
     case RRTE_PRIM_SDF:
         return isect_sdf<NEED_HIT>(pr, SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t_min, t_max, out);
+    case RRTE_PRIM_MESH: return isect_mesh<ANY>(pr, sc.mesh, r, t_min, t_max, out);
     default: return false;
     }
 }
 
 // Compile-time object index (scene-specialised kernel): only the object's
 // own intersector is instantiated.
-template <bool NEED_HIT, class S, uint32_t I>
+template <bool NEED_HIT, class S, uint32_t I, bool ANY = false>
 __device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, float t_min, float t_max, Hit& out) {
     constexpr DPrim pr = S::prims[I];
     constexpr uint32_t kind = pr.kind;
@@ -609,6 +746,7 @@ __device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, f
     else if constexpr (kind == RRTE_PRIM_CAPSULE) return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_SDF)
         return isect_sdf<NEED_HIT>(pr, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_MESH) return isect_mesh<ANY>(pr, sc.mesh, r, t_min, t_max, out);
     else return false;
 }
 
@@ -617,16 +755,19 @@ __device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, f
 // reference, SDF objects march only up to the current closest hit.  The
 // search carries only (t, object); attributes are produced afterwards.
 template <class S>
-__device__ __forceinline__ int closest_t(const S& sc, const Ray& r, float t_min, float& best_t) {
+__device__ __forceinline__ int closest_t(const S& sc, const Ray& r, float t_min, float& best_t, uint32_t& best_sub) {
     int idx = -1;
     best_t = kInf;
+    best_sub = 0u;
     for_each_prim(sc, [&](auto ii) {
         const uint32_t i = ii;
         Hit h;
+        h.sub = 0u;
         float tmax = (prim_at(sc, ii).kind == RRTE_PRIM_SDF && idx >= 0) ? best_t : kInf;
         if (intersect_at<false>(sc, ii, r, t_min, tmax, h)) {
             if (idx < 0 || h.t < best_t) {
                 best_t = h.t;
+                best_sub = h.sub;
                 idx = (int)i;
             }
         }
@@ -641,28 +782,33 @@ __device__ __forceinline__ int closest_t(const S& sc, const Ray& r, float t_min,
 // -> uniform object index -> scalar loads).  Static scene: every object is
 // visited with a compile-time index and skipped unless some lane won it.
 template <class S>
-__device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t, Hit& out) {
+__device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t,
+                                              uint32_t sub, Hit& out) {
     const DPrim& pr = sc.prims[i];
     if (pr.kind == RRTE_PRIM_SDF) sdf_hit_attributes(SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t, out);
+    else if (pr.kind == RRTE_PRIM_MESH) mesh_tri_hit(sc.mesh, sub, r, t_min, kInf, out);
     else intersect_at<true>(sc, i, r, t_min, kInf, out);
 }
 template <class S, uint32_t I>
-__device__ __forceinline__ void attributes_at(const S& sc, UC<I> ii, const Ray& r, float t_min, float t, Hit& out) {
+__device__ __forceinline__ void attributes_at(const S& sc, UC<I> ii, const Ray& r, float t_min, float t, uint32_t sub,
+                                              Hit& out) {
     constexpr DPrim pr = S::prims[I];
     if constexpr (pr.kind == RRTE_PRIM_SDF)
         sdf_hit_attributes(SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t, out);
+    else if constexpr (pr.kind == RRTE_PRIM_MESH)
+        mesh_tri_hit(sc.mesh, sub, r, t_min, kInf, out);
     else
         intersect_at<true>(sc, ii, r, t_min, kInf, out);
 }
 
 template <class S>
-__device__ __forceinline__ void hit_attributes(const S& sc, const Ray& r, float t_min, int idx, float t,
+__device__ __forceinline__ void hit_attributes(const S& sc, const Ray& r, float t_min, int idx, float t, uint32_t sub,
                                                Hit& out) {
     if constexpr (S::kStatic) {
         for_each_prim(sc, [&](auto ii) {
             const uint32_t i = ii;
             if (__any((uint32_t)idx == i)) {
-                if ((uint32_t)idx == i) attributes_at(sc, ii, r, t_min, t, out);
+                if ((uint32_t)idx == i) attributes_at(sc, ii, r, t_min, t, sub, out);
             }
         });
     } else {
@@ -670,7 +816,7 @@ __device__ __forceinline__ void hit_attributes(const S& sc, const Ray& r, float 
         while (pending) {
             const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)idx);
             if ((uint32_t)idx == i) {
-                attributes_at(sc, i, r, t_min, t, out);
+                attributes_at(sc, i, r, t_min, t, sub, out);
                 pending = false;
             }
         }
@@ -680,9 +826,20 @@ __device__ __forceinline__ void hit_attributes(const S& sc, const Ray& r, float 
 template <class S>
 __device__ __forceinline__ int closest_hit(const S& sc, const Ray& r, float t_min, Hit& best) {
     float t;
-    int idx = closest_t(sc, r, t_min, t);
-    hit_attributes(sc, r, t_min, idx, t, best);
+    uint32_t sub;
+    int idx = closest_t(sc, r, t_min, t, sub);
+    hit_attributes(sc, r, t_min, idx, t, sub, best);
     return idx;
+}
+
+// Any-hit form of intersect_at (meshes stop at their first triangle hit).
+template <class S>
+__device__ __forceinline__ bool any_hit_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t_max, Hit& h) {
+    return intersect_at<false, S, true>(sc, i, r, t_min, t_max, h);
+}
+template <class S, uint32_t I>
+__device__ __forceinline__ bool any_hit_at(const S& sc, UC<I> ii, const Ray& r, float t_min, float t_max, Hit& h) {
+    return intersect_at<false, S, I, true>(sc, ii, r, t_min, t_max, h);
 }
 
 // Any hit in [t_min, t_max] (LAMBERT_SHADOW shadow rays).
@@ -694,7 +851,7 @@ __device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min,
         // one wave-uniform skip test: culled, or every lane already occluded (mask cleared)
         if (mask == 0 || (i < 64u && !((mask >> i) & 1ull))) return;
         Hit h;
-        if (!hit_any && intersect_at<false>(sc, ii, r, t_min, t_max, h)) hit_any = true;
+        if (!hit_any && any_hit_at(sc, ii, r, t_min, t_max, h)) hit_any = true;
         if (__all(hit_any)) mask = 0;
     });
     return hit_any;
@@ -723,9 +880,6 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
     return v;
-}
-__device__ __forceinline__ bool finite3(f3 a) {
-    return __builtin_isfinite(a.x) && __builtin_isfinite(a.y) && __builtin_isfinite(a.z);
 }
 __device__ __forceinline__ bool cull_on(const Cull& cl) { return cl.bounds != nullptr && cl.n <= 64u; }
 

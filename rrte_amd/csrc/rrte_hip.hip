@@ -20,6 +20,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "bvh.hpp"
 #include "jit.hpp"
 #include "ray_kernels.hpp"
 
@@ -37,6 +38,12 @@ struct rrte_ctx {
     DLight* d_lights = nullptr; size_t cap_lights = 0;
     rrte_sdf_node* d_nodes = nullptr; size_t cap_nodes = 0;
     float4* d_bounds = nullptr; size_t cap_bounds = 0;  // culling spheres, one per object
+    // triangle meshes: BVH nodes, triangle slots, normals, original-order permutation (bvh.hip)
+    float4* d_mesh_nodes = nullptr; size_t cap_mesh_nodes = 0;
+    float4* d_mesh_tris = nullptr; size_t cap_mesh_tris = 0;
+    float4* d_mesh_norms = nullptr; size_t cap_mesh_norms = 0;
+    uint32_t* d_mesh_perm = nullptr; size_t cap_mesh_perm = 0;
+    MeshView mesh_view{};
     uint32_t n_prims = 0, n_mats = 0, n_lights = 0, n_nodes = 0;
     // frame buffers for the blocking entry points
     uint32_t* d_rgba = nullptr; size_t cap_rgba = 0;
@@ -215,9 +222,17 @@ rrte_status validate(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_para
         (s->num_sdf_nodes && !s->sdf_nodes))
         return fail(c, RRTE_INVALID_ARG, "null array with nonzero count");
     if (s->camera.projection > RRTE_ORTHOGRAPHIC) return fail(c, RRTE_INVALID_ARG, "unknown projection");
+    if ((s->num_mesh_vertices && !s->mesh_vertices) || (s->num_mesh_indices && !s->mesh_indices))
+        return fail(c, RRTE_INVALID_ARG, "null mesh array with nonzero count");
+    if (s->num_mesh_indices % 3) return fail(c, RRTE_INVALID_ARG, "mesh index count not a multiple of 3");
+    if (s->num_mesh_indices / 3 >= (1u << 24)) return fail(c, RRTE_INVALID_ARG, "more than 2^24 mesh triangles");
     for (uint32_t i = 0; i < s->num_prims; ++i) {
         const rrte_prim& pr = s->prims[i];
-        if (pr.kind > RRTE_PRIM_SDF) return fail(c, RRTE_UNSUPPORTED_PRIM, "prim %u: unknown kind %u", i, pr.kind);
+        if (pr.kind > RRTE_PRIM_MESH) return fail(c, RRTE_UNSUPPORTED_PRIM, "prim %u: unknown kind %u", i, pr.kind);
+        if (pr.kind == RRTE_PRIM_MESH) {
+            if ((uint64_t)pr.sdf_first + pr.sdf_count > s->num_mesh_indices / 3)
+                return fail(c, RRTE_INVALID_ARG, "prim %u: mesh triangle range out of bounds", i);
+        }
         if (pr.kind == RRTE_PRIM_SDF) {
             if ((uint64_t)pr.sdf_first + pr.sdf_count > s->num_sdf_nodes)
                 return fail(c, RRTE_INVALID_ARG, "prim %u: SDF node range out of bounds", i);
@@ -339,17 +354,31 @@ void lower_scene(const rrte_scene_ir* s, std::vector<DPrim>& prims, std::vector<
 }
 
 // Upload the scene if it differs from the cached copy (the analogue of
-// caching on Scene::is_dirty, crates/rrte-scene/src/lib.rs:310-312).
+// caching on Scene::is_dirty, crates/rrte-scene/src/lib.rs:310-312).  The key
+// is the IR's bytes; mesh arrays enter it through (addresses, counts,
+// mesh_version), or by content when mesh_version is 0.
+struct MeshKey {
+    const void* v;
+    const void* i;
+    uint64_t nv, ni, version;
+};
+
 rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
     const size_t bp = sizeof(rrte_prim) * s->num_prims, bm = sizeof(rrte_material) * s->num_materials,
                  bl = sizeof(rrte_light) * s->num_lights, bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
-    const size_t key_len = bp + bm + bl + bn + 4 * sizeof(uint32_t);
+    const MeshKey mk{s->mesh_vertices, s->mesh_indices, s->num_mesh_vertices, s->num_mesh_indices, s->mesh_version};
+    const size_t bmv = s->mesh_version ? 0 : sizeof(rrte_mesh_vertex) * s->num_mesh_vertices;
+    const size_t bmi = s->mesh_version ? 0 : sizeof(uint32_t) * s->num_mesh_indices;
+    const size_t key_len = bp + bm + bl + bn + sizeof(MeshKey) + bmv + bmi;
+    const void* parts[] = {s->prims, s->materials, s->lights, s->sdf_nodes, &mk, s->mesh_vertices, s->mesh_indices};
+    const size_t lens[] = {bp, bm, bl, bn, sizeof(MeshKey), bmv, bmi};
     bool same = c->scene_key.size() == key_len;
     if (same) {
         const unsigned char* k = c->scene_key.data();
-        same = (bp == 0 || !memcmp(k, s->prims, bp)) && (bm == 0 || !memcmp(k + bp, s->materials, bm)) &&
-               (bl == 0 || !memcmp(k + bp + bm, s->lights, bl)) &&
-               (bn == 0 || !memcmp(k + bp + bm + bl, s->sdf_nodes, bn));
+        for (int i = 0; i < 7 && same; ++i) {
+            same = lens[i] == 0 || !memcmp(k, parts[i], lens[i]);
+            k += lens[i];
+        }
     }
     *upload_ms = 0.0;
     if (same) {
@@ -359,23 +388,40 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     c->same_scene_renders = 0;
     ++c->scene_gen;
 
+    for (uint32_t k = 0; k < s->num_mesh_indices; ++k)
+        if (s->mesh_indices[k] >= s->num_mesh_vertices)
+            return fail(c, RRTE_INVALID_ARG, "mesh index %u out of range (%u vertices)", k, s->num_mesh_vertices);
     std::vector<DPrim> prims;
     std::vector<DMaterial> mats;
     std::vector<DLight> lights;
     std::vector<float4> bounds;
     lower_scene(s, prims, mats, lights, &bounds);
+    MeshData md;
+    build_mesh_bvhs(s, prims.data(), md, bounds.data());
     rrte_status r;
     if ((r = ensure(c, c->d_prims, c->cap_prims, prims.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_bounds, c->cap_bounds, bounds.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_mats, c->cap_mats, mats.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_lights, c->cap_lights, lights.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_nodes, c->cap_nodes, (size_t)s->num_sdf_nodes)) != RRTE_OK) return r;
+    if ((r = ensure(c, c->d_mesh_nodes, c->cap_mesh_nodes, md.nodes.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, c->d_mesh_tris, c->cap_mesh_tris, md.tris.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, c->d_mesh_norms, c->cap_mesh_norms, md.norms.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, c->d_mesh_perm, c->cap_mesh_perm, md.perm.size())) != RRTE_OK) return r;
     HIPCHK(c, hipEventRecord(c->ev2, st));
-    if (!prims.empty()) HIPCHK(c, hipMemcpyAsync(c->d_prims, prims.data(), prims.size() * sizeof(DPrim), hipMemcpyHostToDevice, st));
-    if (!mats.empty()) HIPCHK(c, hipMemcpyAsync(c->d_mats, mats.data(), mats.size() * sizeof(DMaterial), hipMemcpyHostToDevice, st));
-    if (!lights.empty()) HIPCHK(c, hipMemcpyAsync(c->d_lights, lights.data(), lights.size() * sizeof(DLight), hipMemcpyHostToDevice, st));
-    if (bn) HIPCHK(c, hipMemcpyAsync(c->d_nodes, s->sdf_nodes, bn, hipMemcpyHostToDevice, st));
-    if (!bounds.empty()) HIPCHK(c, hipMemcpyAsync(c->d_bounds, bounds.data(), bounds.size() * sizeof(float4), hipMemcpyHostToDevice, st));
+    auto put = [&](void* dst, const void* src, size_t bytes) -> rrte_status {
+        if (bytes) HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+        return RRTE_OK;
+    };
+    if ((r = put(c->d_prims, prims.data(), prims.size() * sizeof(DPrim))) != RRTE_OK) return r;
+    if ((r = put(c->d_mats, mats.data(), mats.size() * sizeof(DMaterial))) != RRTE_OK) return r;
+    if ((r = put(c->d_lights, lights.data(), lights.size() * sizeof(DLight))) != RRTE_OK) return r;
+    if ((r = put(c->d_nodes, s->sdf_nodes, bn)) != RRTE_OK) return r;
+    if ((r = put(c->d_bounds, bounds.data(), bounds.size() * sizeof(float4))) != RRTE_OK) return r;
+    if ((r = put(c->d_mesh_nodes, md.nodes.data(), md.nodes.size() * sizeof(float4))) != RRTE_OK) return r;
+    if ((r = put(c->d_mesh_tris, md.tris.data(), md.tris.size() * sizeof(float4))) != RRTE_OK) return r;
+    if ((r = put(c->d_mesh_norms, md.norms.data(), md.norms.size() * sizeof(float4))) != RRTE_OK) return r;
+    if ((r = put(c->d_mesh_perm, md.perm.data(), md.perm.size() * sizeof(uint32_t))) != RRTE_OK) return r;
     // the staging vectors die at return: make the copies complete first
     HIPCHK(c, hipStreamSynchronize(st));
     HIPCHK(c, hipEventRecord(c->ev0, st));
@@ -383,6 +429,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, c->ev2, c->ev0);
     *upload_ms = ms;
+    c->mesh_view = MeshView{c->d_mesh_nodes, c->d_mesh_tris, c->d_mesh_norms, c->d_mesh_perm};
     c->h_prims = prims;
     c->h_mats = mats;
     c->h_lights = lights;
@@ -393,10 +440,10 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     c->n_nodes = s->num_sdf_nodes;
     c->scene_key.resize(key_len);
     unsigned char* k = c->scene_key.data();
-    if (bp) memcpy(k, s->prims, bp);
-    if (bm) memcpy(k + bp, s->materials, bm);
-    if (bl) memcpy(k + bp + bm, s->lights, bl);
-    if (bn) memcpy(k + bp + bm + bl, s->sdf_nodes, bn);
+    for (int i = 0; i < 7; ++i) {
+        if (lens[i]) memcpy(k, parts[i], lens[i]);
+        k += lens[i];
+    }
     return RRTE_OK;
 }
 
@@ -514,7 +561,8 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull) {
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
                    uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     KParams k = make_params(c, s, p, rows);
-    SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, s->num_prims, s->num_lights, s->num_materials};
+    SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, s->num_prims, s->num_lights, s->num_materials,
+                 c->mesh_view};
     const bool cull = cull_policy(s, p->mode, c->env_cull);
     Cull cl{cull ? c->d_bounds : nullptr, s->num_prims};
     dim3 grid((p->width + 15) / 16, (rows + 15) / 16), block(256);
@@ -525,7 +573,8 @@ rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params
     c->stats.jit_active = jk ? 1u : 0u;
     if (jk) {
         unsigned long long* ctr = c->d_counters;
-        void* args[] = {&k, &cl, &d_rgba, &d_f32, &ctr};
+        MeshView mv = c->mesh_view;
+        void* args[] = {&k, &cl, &mv, &d_rgba, &d_f32, &ctr};
         HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, 1, 256, 1, 1, 0, st, args, nullptr));
         return RRTE_OK;
     }
@@ -639,8 +688,9 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto& kv : c->jit_cache) jit_release(kv.second);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
-    void* bufs[] = {c->d_prims, c->d_mats,   c->d_lights, c->d_nodes,  c->d_bounds,
-                    c->d_rgba,  c->d_f32,    c->d_counters, c->d_gather, c->d_full};
+    void* bufs[] = {c->d_prims,      c->d_mats,      c->d_lights,     c->d_nodes,     c->d_bounds,
+                    c->d_rgba,       c->d_f32,       c->d_counters,   c->d_gather,    c->d_full,
+                    c->d_mesh_nodes, c->d_mesh_tris, c->d_mesh_norms, c->d_mesh_perm};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (uint32_t* b : c->d_slab)
@@ -726,7 +776,10 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
     std::vector<DPrim> prims;
     std::vector<DMaterial> mats;
     std::vector<DLight> lights;
+    if ((s->num_mesh_indices && !s->mesh_indices) || (s->num_mesh_vertices && !s->mesh_vertices)) return RRTE_INVALID_ARG;
     lower_scene(s, prims, mats, lights);
+    MeshData md;
+    build_mesh_bvhs(s, prims.data(), md, nullptr);
     std::string src = jit_source(prims.data(), (uint32_t)prims.size(), mats.data(), (uint32_t)mats.size(),
                                  lights.data(), (uint32_t)lights.size(), s->sdf_nodes, s->num_sdf_nodes, mode,
                                  cull_policy(s, (uint32_t)mode, env_cull_setting()));

@@ -11,6 +11,7 @@ path behind it.
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 import math
 import os
 from dataclasses import dataclass, field
@@ -756,11 +757,29 @@ class RaytracerConfig:
         return p
 
 
+_MESH_VERSION = itertools.count(1)
+
+
 class _Lowering:
     def __init__(self):
         self.nodes: list = []
         self.materials: list = []
         self._mat_index: dict = {}
+        self.mesh_pos: list = []      # per mesh: (N, 3) float32
+        self.mesh_nrm: list = []
+        self.mesh_idx: list = []      # per mesh: (M, 3) uint32, offset into the shared vertex pool
+        self._nverts = 0
+        self._ntris = 0
+
+    def add_mesh(self, pos, nrm, idx):
+        """Append a mesh to the shared pools; returns (first triangle, triangle count)."""
+        first = self._ntris
+        self.mesh_pos.append(pos)
+        self.mesh_nrm.append(nrm)
+        self.mesh_idx.append(idx.astype(np.uint32) + np.uint32(self._nverts))
+        self._nverts += len(pos)
+        self._ntris += len(idx)
+        return first, len(idx)
 
     def material_index(self, m: Material | None) -> int:
         if m is None:
@@ -794,6 +813,15 @@ class LoweredScene:
         ir.lights, ir.num_lights = self.lights, len(lts)
         ir.sdf_nodes, ir.num_sdf_nodes = self.nodes, len(lw.nodes)
         ir.camera = camera.lower()
+        if lw.mesh_pos:
+            vtx = np.concatenate([np.concatenate([p, n], axis=1) for p, n in zip(lw.mesh_pos, lw.mesh_nrm)])
+            self._mesh_vtx = np.ascontiguousarray(vtx, dtype=np.float32)
+            self._mesh_idx = np.ascontiguousarray(np.concatenate(lw.mesh_idx).reshape(-1), dtype=np.uint32)
+            ir.mesh_vertices = self._mesh_vtx.ctypes.data_as(C.POINTER(abi.MeshVertex))
+            ir.num_mesh_vertices = len(self._mesh_vtx)
+            ir.mesh_indices = self._mesh_idx.ctypes.data_as(C.POINTER(C.c_uint32))
+            ir.num_mesh_indices = len(self._mesh_idx)
+            ir.mesh_version = next(_MESH_VERSION)  # arrays are immutable for this object's lifetime
         self.ir = ir
 
     def ref(self):

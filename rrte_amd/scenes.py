@@ -207,6 +207,26 @@ def deformation_stress(width=3840, height=2160, mode="lambert_shadow", seed=SEED
     return objects, _showcase_lights(), cam, _config(width, height, Color(0.05, 0.05, 0.08, 1.0), mode)
 
 
+def mesh_demo(width=1920, height=1080, mode="lambert_shadow", detail=1.0):
+    """Triangle meshes (§8f rank 4: MeshAsset-shaped data, RRTE_PRIM_MESH): a rolling heightfield
+    terrain, an icosphere, a torus and a second icosphere over the analytic ground sphere, lit by
+    the sdf-showcase lights.  `detail` scales the triangle counts (1.0: ~60 K triangles)."""
+    from .mesh import heightfield, icosphere, torus
+    n = max(8, int(129 * detail ** 0.5))
+    terrain = heightfield((-12.0, 0.0, -12.0), 24.0, n,
+                          lambda x, z: 0.6 * np.sin(0.45 * x) * np.cos(0.35 * z) + 0.25 * np.sin(1.3 * x + 0.7 * z),
+                          LambertianMaterial(Color.rgb(0.45, 0.55, 0.35)))
+    sub = 4 if detail >= 0.5 else 2
+    ball = icosphere((-3.0, 2.2, 0.5), 1.6, sub, LambertianMaterial(Color.rgb(0.8, 0.35, 0.3)))
+    ring = torus((3.0, 2.0, -1.0), 1.6, 0.5, max(12, int(128 * detail ** 0.5)), max(8, int(64 * detail ** 0.5)),
+                 LambertianMaterial(Color.rgb(0.3, 0.5, 0.85)))
+    small = icosphere((0.5, 1.4, 3.0), 0.9, sub - 1, LambertianMaterial(Color.rgb(0.85, 0.8, 0.4)))
+    objects = [Sphere((0.0, -1000.0, 0.0), 1000.0, LambertianMaterial(Color.rgb(0.2, 0.2, 0.2))),
+               terrain, ball, ring, small]
+    cam = _camera(width, height, (0.0, 8.0, 16.0), (0.0, 1.5, 0.0), 45.0)
+    return objects, _showcase_lights(), cam, _config(width, height, Color(0.05, 0.05, 0.08, 1.0), mode)
+
+
 SCENES = {
     "basic-demo": basic_demo,
     "simple-demo": simple_demo,
@@ -214,4 +234,5 @@ SCENES = {
     "sdf-showcase-literal": sdf_showcase_literal,
     "sdf-showcase": sdf_showcase,
     "deformation-stress": deformation_stress,
+    "mesh-demo": mesh_demo,
 }

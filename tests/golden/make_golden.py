@@ -1,6 +1,6 @@
 """Regenerate tests/golden/*.npz from the CPU oracle (run from the repo root):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--force]
 
 The reference ships no golden images; these fixtures freeze the
 oracle's output for every BASELINE scene and both shading modes at small sizes,
@@ -33,7 +33,10 @@ def render_case(name, mode, w, h):
 
 def main():
     out = Path(__file__).resolve().parent
+    force = "--force" in sys.argv  # default: only write fixtures that do not exist yet
     for name, mode, w, h in CASES:
+        if not force and (out / f"{name}_{mode}_{w}x{h}.npz").exists():
+            continue
         img, lin_hash, shadow = render_case(name, mode, w, h)
         np.savez_compressed(out / f"{name}_{mode}_{w}x{h}.npz", rgba8=img, linear_sha256=np.array(lin_hash),
                             shadow_rays=np.array(shadow, np.int64))

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
         assert n in abi.EXPORTS, f"{n} missing from the ctypes mirror"
-    assert lib.rrte_hip_abi_version() == 1
+    assert lib.rrte_hip_abi_version() == 2
 
 
 def test_struct_layouts_match_header_comments():
@@ -34,6 +34,8 @@ def test_struct_layouts_match_header_comments():
     assert C.sizeof(abi.SdfNode) == 64
     assert C.sizeof(abi.Camera) == 80
     assert C.sizeof(abi.RenderParams) == 64
+    assert C.sizeof(abi.MeshVertex) == 24
+    assert C.sizeof(abi.SceneIR) == 4 * 16 + 80 + 2 * 16 + 8  # (pointer, count) pairs, camera, mesh pairs, version
     text = HEADER.read_text()
     for name, size in [("rrte_material", 32), ("rrte_light", 80), ("rrte_sdf_node", 64), ("rrte_camera", 80),
                        ("rrte_render_params", 64)]:
