@@ -1,0 +1,69 @@
+// cpp_mirror_tool — drives the C++ mirror for tests/test_cpp_mirror.py.
+//   cpp_mirror_tool ir <scene> <w> <h> <mode> <out.bin>       lowered IR bytes + render params (no GPU)
+//   cpp_mirror_tool render <scene> <w> <h> <mode> <out.bin>    Raytracer::render_f32(linear): u8 then f32 (GPU)
+//   cpp_mirror_tool errors                                     error behaviour checks (no GPU needed)
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+
+#include "../../rrte_amd/cpp/examples.hpp"
+
+using namespace rrte_renderer;
+
+static Mode parse_mode(const char* m) { return std::strcmp(m, "refcompat") == 0 ? Mode::RefCompat : Mode::LambertShadow; }
+
+int main(int argc, char** argv) {
+    if (argc < 2) return 2;
+    const std::string cmd = argv[1];
+    try {
+        if (cmd == "errors") {
+            int bad = 0;
+            try {  // deformer axes must be coordinate axes
+                twist(Vec3(1.0f, 1.0f, 0.0f), 1.0f);
+                bad |= 1;
+            } catch (const Error& e) {
+                if (e.status != RRTE_UNSUPPORTED_PRIM) bad |= 2;
+            }
+            try {
+                Mesh m({0.0f, 0.0f, 0.0f}, {0u, 1u, 2u});
+                bad |= 4;
+            } catch (const Error& e) {
+                if (e.status != RRTE_INVALID_ARG) bad |= 8;
+            }
+            try {
+                noise(1.0f, 1.0f, rrte_math::ZERO, 0u, RRTE_SDF_MAX_OCTAVES + 1u);
+                bad |= 16;
+            } catch (const Error&) {
+            }
+            std::printf("errors %d\n", bad);
+            return bad ? 1 : 0;
+        }
+        if (argc < 7) return 2;
+        const auto sc = rrte_examples::by_name(argv[2], (uint32_t)std::atoi(argv[3]), (uint32_t)std::atoi(argv[4]),
+                                               parse_mode(argv[5]));
+        std::ofstream out(argv[6], std::ios::binary);
+        if (cmd == "ir") {
+            const LoweredScene ls(sc.objects, sc.lights, sc.camera);
+            const auto b = ls.bytes();
+            const rrte_render_params p = sc.config.lower();
+            out.write(reinterpret_cast<const char*>(b.data()), (std::streamsize)b.size());
+            out.write(reinterpret_cast<const char*>(&p), sizeof p);
+            return 0;
+        }
+        if (cmd == "render") {
+            Raytracer rt(sc.config, 0);
+            const auto u8 = rt.render(sc.objects, sc.lights, {}, sc.camera);
+            const auto pr = rt.render_f32(sc.objects, sc.lights, sc.camera, /*linear=*/true);
+            out.write(reinterpret_cast<const char*>(u8.data()), (std::streamsize)u8.size());
+            out.write(reinterpret_cast<const char*>(pr.second.data()), (std::streamsize)(pr.second.size() * 4));
+            const rrte_stats st = rt.stats();
+            std::printf("shadow_rays %llu\n", (unsigned long long)st.shadow_rays);
+            return 0;
+        }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+    return 2;
+}
