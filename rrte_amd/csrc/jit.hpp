@@ -17,9 +17,10 @@ struct JitKernel {
 };
 
 // HIP source for one scene + shading mode: the scene as static constexpr arrays
-// and an extern "C" rrte_jit_kernel instantiating ray_kernel_body<mode, Scene, true, cull>.
+// and an extern "C" rrte_jit_kernel instantiating ray_kernel_body<mode, Scene, single, cull>
+// (single: one sample, one bounce -> straight-line code; else runtime sample/bounce loops).
 std::string jit_source(const DPrim* prims, uint32_t np, const DMaterial* mats, uint32_t nm, const DLight* lights,
-                       uint32_t nl, const rrte_sdf_node* nodes, uint32_t nn, int mode, bool cull);
+                       uint32_t nl, const rrte_sdf_node* nodes, uint32_t nn, int mode, bool cull, bool single);
 
 // hiprtc compile for gfx950 + module load.  On failure `log` holds the reason.
 bool jit_compile(const std::string& src, JitKernel& out, std::string& log);

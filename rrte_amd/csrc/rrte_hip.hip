@@ -75,7 +75,7 @@ struct rrte_ctx {
     bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
     int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
-    struct { uint64_t gen; int mode, jit_mode; bool cull, valid; JitKernel* k; } jit_last{};
+    struct { uint64_t gen; int mode, jit_mode; bool cull, single, valid; JitKernel* k; } jit_last{};
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
     std::vector<DPrim> h_prims;                  // host copy of the lowered scene (JIT source)
     std::vector<DMaterial> h_mats;
@@ -516,20 +516,23 @@ bool cull_policy(const rrte_scene_ir* s, uint32_t mode, int env_cull) {
 // JIT policy says so; nullptr = use the generic kernel.
 constexpr uint32_t kJitMaxPrims = 128, kJitMaxNodes = 1024;
 
-JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull) {
+JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
     if (c->jit_mode == RRTE_JIT_OFF) return nullptr;
     auto& last = c->jit_last;  // per-frame fast path: same scene, mode and policy as the last frame
-    if (last.valid && last.gen == c->scene_gen && last.mode == mode && last.cull == cull && last.jit_mode == c->jit_mode)
+    if (last.valid && last.gen == c->scene_gen && last.mode == mode && last.cull == cull && last.single == single &&
+        last.jit_mode == c->jit_mode)
         return last.k;
     if (c->h_prims.size() > kJitMaxPrims || c->h_nodes.size() > kJitMaxNodes) return nullptr;
     std::string key(c->scene_key.begin(), c->scene_key.end());
     key.push_back((char)mode);
     key.push_back((char)cull);
+    key.push_back((char)single);
     auto remember = [&](JitKernel* k) {
         last.gen = c->scene_gen;
         last.mode = mode;
         last.jit_mode = c->jit_mode;
         last.cull = cull;
+        last.single = single;
         last.k = k;
         last.valid = true;
         return k;
@@ -544,7 +547,7 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull) {
     }
     std::string src = jit_source(c->h_prims.data(), (uint32_t)c->h_prims.size(), c->h_mats.data(),
                                  (uint32_t)c->h_mats.size(), c->h_lights.data(), (uint32_t)c->h_lights.size(),
-                                 c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull);
+                                 c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull, single);
     JitKernel jk;
     std::string log;
     if (hipSetDevice(c->device) != hipSuccess || !jit_compile(src, jk, log)) {
@@ -567,9 +570,10 @@ rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params
     Cull cl{cull ? c->d_bounds : nullptr, s->num_prims};
     dim3 grid((p->width + 15) / 16, (rows + 15) / 16), block(256);
     if (rows == 0) return RRTE_OK;
-    // specialised kernels are single-sample, single-bounce (see ray_color<SINGLE>)
+    // single-sample, single-bounce frames get the straight-line specialisation (SINGLE); others the
+    // specialisation with runtime sample / bounce loops
     const bool single = p->samples_per_pixel == 1 && (p->mode == RRTE_MODE_LAMBERT_SHADOW || p->max_depth <= 1);
-    JitKernel* jk = single ? jit_kernel_for(c, (int)p->mode, cull) : nullptr;
+    JitKernel* jk = jit_kernel_for(c, (int)p->mode, cull, single);
     c->stats.jit_active = jk ? 1u : 0u;
     if (jk) {
         unsigned long long* ctr = c->d_counters;
@@ -782,7 +786,7 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
     build_mesh_bvhs(s, prims.data(), md, nullptr);
     std::string src = jit_source(prims.data(), (uint32_t)prims.size(), mats.data(), (uint32_t)mats.size(),
                                  lights.data(), (uint32_t)lights.size(), s->sdf_nodes, s->num_sdf_nodes, mode,
-                                 cull_policy(s, (uint32_t)mode, env_cull_setting()));
+                                 cull_policy(s, (uint32_t)mode, env_cull_setting()), true);
     std::string msg;
     bool ok = jit_compile_only(src, msg);
     if (log && log_len) {

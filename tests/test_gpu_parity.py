@@ -40,8 +40,7 @@ def compare(objs, lights, cam, cfg, linear_exact=True, threads=16, jit=abi.JIT_O
     assert u8 <= 1, info
     assert int(st.shadow_rays) == rsh, info
     assert st.primary_rays == cfg.width * cfg.height * cfg.samples_per_pixel
-    single = cfg.samples_per_pixel == 1 and (cfg.mode == "lambert_shadow" or cfg.max_depth <= 1)
-    assert st.jit_active == (1 if (jit == abi.JIT_ON and single) else 0), "unexpected kernel path"
+    assert st.jit_active == (1 if jit == abi.JIT_ON else 0), "unexpected kernel path"
     if linear_exact:
         assert np.array_equal(glin.view(np.uint32), rlin.view(np.uint32)), info
     return info
@@ -130,12 +129,22 @@ def test_shadow_culling_is_exact(case, jit, monkeypatch):
     assert out["0"][1] == out["1"][1]
 
 
-def test_stochastic_multibounce_materials():
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+def test_stochastic_multibounce_materials(jit):
     """Reference default workload shape: spp > 1, random jitter, depth > 1, Lambertian/Metal/
     Dielectric/Emissive scatter (§8f rank 1).  Same counter-based RNG stream on both sides;
-    the device accumulates the recursion forward (rounding-level differences beyond depth 2)."""
+    the device accumulates the recursion forward (rounding-level differences beyond depth 2).
+    JIT_ON: the scene-specialised kernel with runtime sample/bounce loops."""
     objs, lights, cam, cfg = se.materials_scene(160, 100, spp=4, depth=8)
-    compare(objs, lights, cam, cfg, linear_exact=False)
+    compare(objs, lights, cam, cfg, linear_exact=False, jit=jit)
+
+
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+def test_stock_config_depth2_is_bit_exact(jit):
+    """spp 4, random jitter and scatter, depth 2 (forward accumulation is exact up to depth 2)."""
+    objs, lights, cam, cfg = scenes.sdf_showcase(160, 90, mode="refcompat")
+    cfg.samples_per_pixel, cfg.max_depth, cfg.jitter = 4, 2, "random"
+    compare(objs, lights, cam, cfg, jit=jit)
 
 
 @pytest.mark.parametrize("w,h", [(1, 1), (17, 13), (64, 1), (1, 64), (33, 47)])
