@@ -2,10 +2,11 @@
 //
 // A mesh is defined as the Vec<Triangle> it stands for (include/rrte_hip.h): closest hit over
 // its triangles in index order.  The device finds the same hit through a BVH: binned-SAH build
-// (16 bins per axis, leaves of <= 4 triangles, depth < kMeshStack), children of a node stored
-// next to each other, node boxes inflated so that a triangle's Moller-Trumbore hit point -- which
-// f32 rounding can put marginally outside the triangle -- always lies inside every box on its
-// path, and ties broken by the original triangle index.  Triangles are stored in leaf order with
+// (16 bins per axis, leaves of <= 4 triangles; index-median splits below depth 20, depth < 32 =
+// the device stack), one 64-byte record per interior node holding BOTH children's boxes and links
+// (the traversal tests the two children together and descends into the nearer), boxes inflated
+// so that a triangle's Moller-Trumbore hit point -- which f32 rounding can put marginally outside
+// the triangle -- always lies inside every box on its path, and ties broken by the original index.  Triangles are stored in leaf order with
 // e1 = v1 - v0 and e2 = v2 - v0 precomputed (the same f32 subtractions the test performs).
 #include "bvh.hpp"
 
@@ -18,7 +19,6 @@ namespace {
 
 constexpr int kBins = 16;
 constexpr uint32_t kLeafMax = 4;
-constexpr uint32_t kMaxDepth = 28;  // < kMeshStack (32) in ray_kernels.hpp
 
 struct Box {
     float lo[3] = {INFINITY, INFINITY, INFINITY};
@@ -48,21 +48,21 @@ struct BTri {
     uint32_t orig;
 };
 
+// Links: interior record index (bit 31 clear), or a leaf: bit 31 set, triangle count - 1 in bits
+// 24-30 (1..128 triangles), first triangle slot (mesh-local) in bits 0-23.
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kSahDepth = 20;     // SAH splits above this depth, index-median splits below
+constexpr uint32_t kMaxDepth = 31;     // < kMeshStack (32) in ray_kernels.hpp
+constexpr uint32_t kBigLeaf = 128;
+
 struct Builder {
     std::vector<BTri>& t;
-    std::vector<Box> boxes;       // per node (inflated), filled bottom-up
-    std::vector<uint32_t> meta;   // per node: leaf count or 0x80000000 | axis
-    std::vector<uint32_t> first;  // per node: first child / first triangle (local)
+    struct Rec { Box b[2]; uint32_t link[2]; uint32_t axis; };
+    std::vector<Rec> recs;
     uint32_t depth_max = 0;
+    bool too_deep = false;
 
     explicit Builder(std::vector<BTri>& tris) : t(tris) {}
-
-    uint32_t alloc() {
-        boxes.emplace_back();
-        meta.push_back(0);
-        first.push_back(0);
-        return (uint32_t)boxes.size() - 1;
-    }
 
     // Inflation: 1 % of the leaf's extent plus a relative term on its coordinates.
     static Box inflate(Box b) {
@@ -79,73 +79,62 @@ struct Builder {
         return b;
     }
 
-    void build(uint32_t node, uint32_t b, uint32_t e, uint32_t depth) {
+    // Builds the subtree over t[b, e); returns its link and (inflated) box.
+    std::pair<uint32_t, Box> build(uint32_t b, uint32_t e, uint32_t depth) {
         depth_max = std::max(depth_max, depth);
-        Box cb;  // centroid bounds
-        Box nb;
+        Box cb, nb;
         for (uint32_t i = b; i < e; ++i) {
             cb.grow(t[i].c);
             nb.grow(t[i].box);
         }
         const uint32_t n = e - b;
-        auto make_leaf = [&]() {
-            boxes[node] = inflate(nb);
-            meta[node] = n;
-            first[node] = b;
-        };
-        if (n <= kLeafMax || depth >= kMaxDepth) {
-            if (n > kLeafMax && depth >= kMaxDepth) {  // depth cap: split by index into a leaf chain is not
-                make_leaf();                          // possible without more depth; keep one big leaf
-                return;
-            }
-            make_leaf();
-            return;
+        if (n <= kLeafMax || (depth >= kMaxDepth && n <= kBigLeaf)) return {kLeafBit | ((n - 1) << 24) | b, inflate(nb)};
+        if (depth >= kMaxDepth) {  // cannot happen for SAH-then-median trees below 2^24 triangles
+            too_deep = true;
+            return {kLeafBit | ((kBigLeaf - 1) << 24) | b, inflate(nb)};
         }
-        // binned SAH
-        float best_cost = INFINITY;
-        int best_axis = -1, best_bin = -1;
-        for (int axis = 0; axis < 3; ++axis) {
-            const float lo = cb.lo[axis], ext = cb.hi[axis] - cb.lo[axis];
-            if (!(ext > 0.0f)) continue;
-            Box bb[kBins];
-            uint32_t cnt[kBins] = {};
-            for (uint32_t i = b; i < e; ++i) {
-                int k = (int)((t[i].c[axis] - lo) / ext * kBins);
-                k = std::min(std::max(k, 0), kBins - 1);
-                bb[k].grow(t[i].box);
-                ++cnt[k];
-            }
-            Box left[kBins];
-            uint32_t lc[kBins];
-            Box acc;
-            uint32_t ac = 0;
-            for (int k = 0; k < kBins; ++k) {
-                acc.grow(bb[k]);
-                ac += cnt[k];
-                left[k] = acc;
-                lc[k] = ac;
-            }
-            Box racc;
-            uint32_t rc = 0;
-            for (int k = kBins - 1; k > 0; --k) {
-                racc.grow(bb[k]);
-                rc += cnt[k];
-                const uint32_t l = lc[k - 1];
-                if (l == 0 || rc == 0) continue;
-                const float cost = left[k - 1].area() * (float)l + racc.area() * (float)rc;
-                if (cost < best_cost) {
-                    best_cost = cost;
-                    best_axis = axis;
-                    best_bin = k;
+        int axis = -1, best_bin = -1;
+        if (depth < kSahDepth) {  // binned SAH
+            float best_cost = INFINITY;
+            for (int ax = 0; ax < 3; ++ax) {
+                const float lo = cb.lo[ax], ext = cb.hi[ax] - cb.lo[ax];
+                if (!(ext > 0.0f)) continue;
+                Box bb[kBins];
+                uint32_t cnt[kBins] = {};
+                for (uint32_t i = b; i < e; ++i) {
+                    int k = (int)((t[i].c[ax] - lo) / ext * kBins);
+                    k = std::min(std::max(k, 0), kBins - 1);
+                    bb[k].grow(t[i].box);
+                    ++cnt[k];
+                }
+                Box left[kBins];
+                uint32_t lc[kBins];
+                Box acc;
+                uint32_t ac = 0;
+                for (int k = 0; k < kBins; ++k) {
+                    acc.grow(bb[k]);
+                    ac += cnt[k];
+                    left[k] = acc;
+                    lc[k] = ac;
+                }
+                Box racc;
+                uint32_t rc = 0;
+                for (int k = kBins - 1; k > 0; --k) {
+                    racc.grow(bb[k]);
+                    rc += cnt[k];
+                    const uint32_t l = lc[k - 1];
+                    if (l == 0 || rc == 0) continue;
+                    const float cost = left[k - 1].area() * (float)l + racc.area() * (float)rc;
+                    if (cost < best_cost) {
+                        best_cost = cost;
+                        axis = ax;
+                        best_bin = k;
+                    }
                 }
             }
         }
-        uint32_t mid;
-        int axis = best_axis;
-        if (axis < 0) {  // all centroids coincide: split by index
-            axis = 0;
-            mid = b + n / 2;
-        } else {
+        uint32_t mid = b + n / 2;
+        if (axis >= 0) {
             const float lo = cb.lo[axis], ext = cb.hi[axis] - cb.lo[axis];
             auto it = std::partition(t.begin() + b, t.begin() + e, [&](const BTri& x) {
                 int k = (int)((x.c[axis] - lo) / ext * kBins);
@@ -154,17 +143,26 @@ struct Builder {
             });
             mid = (uint32_t)(it - t.begin());
             if (mid == b || mid == e) mid = b + n / 2;
+        } else {  // index-median split along the widest centroid axis
+            axis = 0;
+            for (int ax = 1; ax < 3; ++ax)
+                if (cb.hi[ax] - cb.lo[ax] > cb.hi[axis] - cb.lo[axis]) axis = ax;
+            std::nth_element(t.begin() + b, t.begin() + mid, t.begin() + e,
+                             [&](const BTri& x, const BTri& y) { return x.c[axis] < y.c[axis]; });
         }
-        const uint32_t l = alloc();
-        const uint32_t r = alloc();
-        (void)r;
-        meta[node] = 0x80000000u | (uint32_t)axis;
-        first[node] = l;
-        build(l, b, mid, depth + 1);
-        build(l + 1, mid, e, depth + 1);
-        Box u = boxes[l];
-        u.grow(boxes[l + 1]);
-        boxes[node] = u;  // children are inflated already
+        const uint32_t r = (uint32_t)recs.size();
+        recs.emplace_back();
+        auto L = build(b, mid, depth + 1);
+        auto R = build(mid, e, depth + 1);
+        Rec& rec = recs[r];
+        rec.b[0] = L.second;
+        rec.b[1] = R.second;
+        rec.link[0] = L.first;
+        rec.link[1] = R.first;
+        rec.axis = (uint32_t)axis;
+        Box u = L.second;
+        u.grow(R.second);
+        return {r, u};
     }
 };
 
@@ -191,23 +189,21 @@ void build_mesh_bvhs(const rrte_scene_ir* s, DPrim* prims, MeshData& out, float4
             for (int a = 0; a < 3; ++a) bt.c[a] = 0.5f * (bt.box.lo[a] + bt.box.hi[a]);
             bt.orig = k;
         }
-        const uint32_t node_base = (uint32_t)(out.nodes.size() / 2);
+        const uint32_t rec_base = (uint32_t)(out.nodes.size() / 4);
         const uint32_t slot_base = (uint32_t)(out.tris.size() / 3);
         Builder bd(tris);
-        const uint32_t root = bd.alloc();
-        if (ntri) {
-            bd.build(root, 0, ntri, 0);
-        } else {
-            bd.boxes[root] = Box();  // empty: a box no ray enters
-            bd.meta[root] = 0;
-        }
+        std::pair<uint32_t, Box> root{kLeafBit, Box()};  // empty mesh: a leaf with no triangles (count field unused)
+        if (ntri) root = bd.build(0, ntri, 0);
         out.max_depth = std::max(out.max_depth, bd.depth_max);
-        for (size_t k = 0; k < bd.boxes.size(); ++k) {
-            const Box& b = bd.boxes[k];
-            const bool leaf = !(bd.meta[k] & 0x80000000u);
-            const uint32_t a = leaf ? slot_base + bd.first[k] : node_base + bd.first[k];
-            out.nodes.push_back(f4(b.lo[0], b.lo[1], b.lo[2], bits_f(a)));
-            out.nodes.push_back(f4(b.hi[0], b.hi[1], b.hi[2], bits_f(bd.meta[k])));
+        out.too_deep = out.too_deep || bd.too_deep;
+        // globalise links: interior -> rec_base + r; leaf -> slot_base + first
+        auto glob = [&](uint32_t link) { return (link & kLeafBit) ? link + slot_base : link + rec_base; };
+        for (const auto& rc : bd.recs) {
+            // record: child 0 box (w = child 0 link), child 1 box (w = child 1 link), 4 x float4
+            out.nodes.push_back(f4(rc.b[0].lo[0], rc.b[0].lo[1], rc.b[0].lo[2], bits_f(glob(rc.link[0]))));
+            out.nodes.push_back(f4(rc.b[0].hi[0], rc.b[0].hi[1], rc.b[0].hi[2], bits_f(rc.axis)));
+            out.nodes.push_back(f4(rc.b[1].lo[0], rc.b[1].lo[1], rc.b[1].lo[2], bits_f(glob(rc.link[1]))));
+            out.nodes.push_back(f4(rc.b[1].hi[0], rc.b[1].hi[1], rc.b[1].hi[2], 0.0f));
         }
         out.perm.resize(slot_base + ntri);
         for (uint32_t k = 0; k < ntri; ++k) {
@@ -225,11 +221,11 @@ void build_mesh_bvhs(const rrte_scene_ir* s, DPrim* prims, MeshData& out, float4
             out.perm[slot_base + o] = slot_base + k;
         }
         DPrim& d = prims[pi];
-        d.sdf_first = node_base + root;
+        d.sdf_first = ntri ? glob(root.first) : kLeafBit;  // root link (an empty mesh: no triangles at all)
         d.sdf_count = ntri;
         d.p[0] = (float)slot_base;
         if (bounds) {
-            const Box& b = bd.boxes[root];
+            const Box& b = root.second;
             double c[3], r2 = 0.0;
             for (int a = 0; a < 3; ++a) {
                 c[a] = 0.5 * ((double)b.lo[a] + b.hi[a]);

@@ -21,12 +21,13 @@ constexpr uint32_t kCounterStride = 16;   // u64 per shard: one 128-B line each
 // members are static constexpr arrays and counts: the same device code below
 // then fully unrolls its object / node / light loops and folds every scene
 // constant into the instruction stream.
-// Triangle-mesh data (RRTE_PRIM_MESH), built once per scene on the host (rrte_hip.hip,
-// build_mesh_bvh).  BVH node k = nodes[2k] (box min xyz, w = first child / first triangle slot)
-// and nodes[2k+1] (box max xyz, w = bit 31 set: interior, split axis in bits 0-1, children a and
-// a+1; else leaf triangle count).  Triangle slot k = tris[3k..3k+2]: v0 (w = the triangle's
-// index within its mesh), e1 = v1-v0, e2 = v2-v0; norms[3k..3k+2] = vertex normals.  perm maps
-// (mesh's first slot + original index) -> slot, for the original-order scan.
+// Triangle-mesh data (RRTE_PRIM_MESH), built once per scene on the host (bvh.hip).  A link is an
+// interior record index (bit 31 clear) or a leaf (bit 31 set, triangle count - 1 in bits 24-30,
+// first triangle slot in bits 0-23).  Interior record k = nodes[4k..4k+3]: child 0 box min (w =
+// child 0 link), child 0 box max (w = split axis), child 1 box min (w = child 1 link), child 1 box
+// max.  Triangle slot k = tris[3k..3k+2]: v0 (w = the triangle's index within its mesh), e1 = v1-v0,
+// e2 = v2-v0; norms[3k..3k+2] = vertex normals.  perm maps (mesh's first slot + original index) ->
+// slot, for the original-order scan.
 struct MeshView {
     const float4* __restrict__ nodes;
     const float4* __restrict__ tris;
@@ -672,20 +673,33 @@ __device__ __forceinline__ bool isect_mesh(const DPrim& pr, const MeshView& mv, 
         const f3 inv = V(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
         uint32_t* stk = mesh_stack();
         int sp = 0;
-        uint32_t node = pr.sdf_first;
-        for (;;) {
-            const float4 lo = mv.nodes[2 * node], hi = mv.nodes[2 * node + 1];
-            if (box_entry(lo, hi, r.o, inv, t_min, found ? fminf(best, t_max) : t_max) != kInf) {
-                const uint32_t meta = __float_as_uint(hi.w), a = __float_as_uint(lo.w);
-                if (meta & 0x80000000u) {  // interior: near child first (sign of d on the split axis)
-                    const uint32_t axis = meta & 3u;
-                    const float da = axis == 0u ? r.d.x : (axis == 1u ? r.d.y : r.d.z);
-                    const bool lfirst = !(da < 0.0f);
-                    stk[(sp++) * 256] = lfirst ? a + 1u : a;
-                    node = lfirst ? a : a + 1u;
+        uint32_t link = count ? pr.sdf_first : 0u;
+        while (count) {
+            if (!(link & 0x80000000u)) {
+                // interior: test both children, descend into the nearer, keep the farther
+                const float4* rec = mv.nodes + 4u * link;
+                const float4 l0 = rec[0], h0 = rec[1], l1 = rec[2], h1 = rec[3];
+                const float cap = found ? fminf(best, t_max) : t_max;
+                const float t0 = box_entry(l0, h0, r.o, inv, t_min, cap);
+                const float t1 = box_entry(l1, h1, r.o, inv, t_min, cap);
+                const uint32_t c0 = __float_as_uint(l0.w), c1 = __float_as_uint(l1.w);
+                if (t0 != kInf && t1 != kInf) {
+                    const bool near0 = t0 <= t1;
+                    stk[(sp++) * 256] = near0 ? c1 : c0;
+                    link = near0 ? c0 : c1;
                     continue;
                 }
-                for (uint32_t k = a; k < a + meta; ++k) {
+                if (t0 != kInf) {
+                    link = c0;
+                    continue;
+                }
+                if (t1 != kInf) {
+                    link = c1;
+                    continue;
+                }
+            } else {
+                const uint32_t a = link & 0xFFFFFFu, n = ((link >> 24) & 0x7Fu) + 1u;
+                for (uint32_t k = a; k < a + n; ++k) {
                     const float4 A = mv.tris[3 * k];
                     float t, u, v;
                     if (mt_test(xyz(A), xyz(mv.tris[3 * k + 1]), xyz(mv.tris[3 * k + 2]), r, t_min, t_max, t, u, v)) {
@@ -702,7 +716,7 @@ __device__ __forceinline__ bool isect_mesh(const DPrim& pr, const MeshView& mv, 
                 if (ANY && found) break;
             }
             if (sp == 0) break;
-            node = stk[(--sp) * 256];
+            link = stk[(--sp) * 256];
         }
     }
     out.t = best;

@@ -398,6 +398,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     lower_scene(s, prims, mats, lights, &bounds);
     MeshData md;
     build_mesh_bvhs(s, prims.data(), md, bounds.data());
+    if (md.too_deep) return fail(c, RRTE_UNSUPPORTED_PRIM, "mesh BVH deeper than the traversal stack");
     rrte_status r;
     if ((r = ensure(c, c->d_prims, c->cap_prims, prims.size())) != RRTE_OK) return r;
     if ((r = ensure(c, c->d_bounds, c->cap_bounds, bounds.size())) != RRTE_OK) return r;
