@@ -68,6 +68,16 @@ def cpu_threads():
     return min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(scene, params, budget_s, stock=None):
     """The oracle (C restatement of Raytracer::render) on this host's cores (SURVEY §8d):
     N threads: median of up to 5 whole frames after 1 warm-up; 1 thread: one whole frame (or a
@@ -89,6 +99,7 @@ def cpu_baseline(scene, params, budget_s, stock=None):
     rays = W * H * params.samples_per_pixel + shadow
     out = {
         "value": rays / med / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
+        "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
         "sample": f"median of {len(times)} whole {W}x{H} frames (1 warm-up) of the same scene/mode, "
                   f"{med * 1e3:.1f} ms/frame, oracle/rrte_oracle.c -O3 -march=x86-64-v3, {threads} threads",
     }
