@@ -21,9 +21,10 @@ from pathlib import Path
 import numpy as np
 
 # Frames in flight need their streams on distinct hardware queues; HIP's default of 4 per
-# process is shared with torch's and the library's own streams (measured: 4 -> 8 queues takes an
-# N=8 rank's frame from 40 to 24 us at 4 frames in flight).  Must be set before HIP starts.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# process is shared with torch's and the library's own streams (measured, tools/inflight_sweep.sh:
+# an N=8 rank's frame takes 40 us with 4 queues / 4 frames, 24 us with 8 / 4, 20 us with 16 / 8).
+# Must be set before HIP starts.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -48,7 +49,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stock", action="store_true", help="skip the stock-config secondary measurement")
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=8,
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
                          "so one frame's tail overlaps the next frame's start (1 = strictly one after another)")
     ap.add_argument("--no-overlap", action="store_true",
