@@ -56,8 +56,13 @@ struct rrte_ctx {
     int nranks = 1, rank = 0;
     uint32_t* d_gather = nullptr; size_t cap_gather = 0;
     uint32_t* d_full = nullptr; size_t cap_full = 0;
-    // pipelined gather (RRTE_FLAG_GATHER_OVERLAP): comm stream + two slabs, event-ordered
-    hipStream_t cstream = nullptr;
+    // pipelined gather (RRTE_FLAG_GATHER_OVERLAP): consecutive frames alternate between two
+    // communicators (the second split from the first) on two comm streams, so the gathers of
+    // neighbouring frames overlap; slabs are a ring, everything event-ordered
+    static constexpr int kComms = 2;
+    int ncomms = 1;  // RRTE_GATHER_COMMS=2 enables the second communicator (opt-in: see comm_init)
+    ncclComm_t gcomm[kComms] = {};
+    hipStream_t gstream[kComms] = {};
     static constexpr int kSlabs = 16;  // frames whose gather may be in flight at once
     hipEvent_t ev_rend[kSlabs] = {}, ev_gath[kSlabs] = {};
     uint32_t* d_slab[kSlabs] = {};
@@ -391,6 +396,8 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     for (uint32_t k = 0; k < s->num_mesh_indices; ++k)
         if (s->mesh_indices[k] >= s->num_mesh_vertices)
             return fail(c, RRTE_INVALID_ARG, "mesh index %u out of range (%u vertices)", k, s->num_mesh_vertices);
+    // frames still in flight (possibly on other streams) read the current scene buffers
+    HIPCHK(c, hipDeviceSynchronize());
     std::vector<DPrim> prims;
     std::vector<DMaterial> mats;
     std::vector<DLight> lights;
@@ -690,9 +697,11 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->gcomm[1] && c->gcomm[1] != c->comm) ncclCommDestroy(c->gcomm[1]);
     if (c->comm) ncclCommDestroy(c->comm);
     for (auto& kv : c->jit_cache) jit_release(kv.second);
-    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    for (hipStream_t gs : c->gstream)
+        if (gs) (void)hipStreamSynchronize(gs);
     void* bufs[] = {c->d_prims,      c->d_mats,      c->d_lights,     c->d_nodes,     c->d_bounds,
                     c->d_rgba,       c->d_f32,       c->d_counters,   c->d_gather,    c->d_full,
                     c->d_mesh_nodes, c->d_mesh_tris, c->d_mesh_norms, c->d_mesh_perm};
@@ -708,7 +717,8 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (c->ev_rend[i]) (void)hipEventDestroy(c->ev_rend[i]);
         if (c->ev_gath[i]) (void)hipEventDestroy(c->ev_gath[i]);
     }
-    if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    for (hipStream_t gs : c->gstream)
+        if (gs) (void)hipStreamDestroy(gs);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -816,9 +826,19 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
         ncclCommDestroy(c->comm);
         c->comm = nullptr;
     }
+    if (c->gcomm[1] && c->gcomm[1] != c->comm) ncclCommDestroy(c->gcomm[1]);
+    c->gcomm[0] = c->gcomm[1] = nullptr;
     ncclUniqueId id;
     memcpy(&id, id_bytes, sizeof id);
     NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    // Optional second communicator over the same ranks (collective: every rank calls comm_init),
+    // so the pipelined gathers of neighbouring frames can overlap.  Opt-in: two communicators
+    // running concurrently are only deadlock-free while both their kernels can be resident at
+    // once, which this repository could not verify on more than one GPU.
+    const char* nc = getenv("RRTE_GATHER_COMMS");
+    c->ncomms = (nc && nc[0] == '2') ? 2 : 1;
+    if (c->ncomms == 2) NCCLCHK(c, ncclCommSplit(c->comm, 0, rank, &c->gcomm[1], nullptr));
+    c->gcomm[0] = c->comm;
     c->nranks = nranks;
     c->rank = rank;
     return RRTE_OK;
@@ -848,46 +868,61 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
     }
     if (!c->comm) return fail(c, RRTE_INVALID_ARG, "rrte_hip_comm_init has not been called");
     const dim3 dg((p->width + 255) / 256 < 8 ? (p->width + 255) / 256 : 8, p->height);
+    if (!c->ev_rend[0]) {
+        for (int i = 0; i < rrte_ctx::kComms; ++i) HIPCHK(c, hipStreamCreateWithFlags(&c->gstream[i], hipStreamNonBlocking));
+        for (int i = 0; i < rrte_ctx::kSlabs; ++i) {
+            HIPCHK(c, hipEventCreateWithFlags(&c->ev_rend[i], hipEventDisableTiming));
+            HIPCHK(c, hipEventCreateWithFlags(&c->ev_gath[i], hipEventDisableTiming));
+        }
+    }
+    // slabs are a ring shared by every frame in flight, whatever stream it comes on: a frame
+    // waits until the previous user of its slab has been gathered
+    const int slot = (int)(c->gather_frames % rrte_ctx::kSlabs);
+    if (c->cap_slab[slot] < slice * (size_t)c->nranks) HIPCHK(c, hipDeviceSynchronize());
+    if ((r = ensure(c, c->d_slab[slot], c->cap_slab[slot], slice * (size_t)c->nranks)) != RRTE_OK) return r;
+    uint32_t* slab = c->d_slab[slot];
+    uint32_t* mine = slab + (size_t)c->rank * slice;  // in-place send slot
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[slot], 0));
     if (!(p->flags & RRTE_FLAG_GATHER_OVERLAP)) {
-        // everything on `st`: render this rank's bands into its slot, gather in place, de-interleave
-        if ((r = ensure(c, c->d_gather, c->cap_gather, slice * (size_t)c->nranks)) != RRTE_OK) return r;
-        uint32_t* mine = c->d_gather + (size_t)c->rank * slice;  // in-place send slot
+        // everything on `st`: render this rank's bands into its slot, gather in place, de-interleave.
+        // Gathers on one communicator must run in the same order on every rank: when frames come
+        // on several streams, each waits for the previous frame's gather.
         if ((r = launch(c, s, &pp, rows, mine, nullptr, st)) != RRTE_OK) return r;
         HIPCHK(c, hipEventRecord(c->ev1, st));
-        NCCLCHK(c, ncclGather(mine, c->d_gather, slice * 4, ncclUint8, root, c->comm, st));
+        if (c->gather_frames > 0)
+            HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[(c->gather_frames - 1) % rrte_ctx::kSlabs], 0));
+        NCCLCHK(c, ncclGather(mine, slab, slice * 4, ncclUint8, root, c->comm, st));
         if (c->rank == root) {
-            hipLaunchKernelGGL(deinterleave_kernel, dg, dim3(256), 0, st, c->d_gather, static_cast<uint32_t*>(d_full),
+            hipLaunchKernelGGL(deinterleave_kernel, dg, dim3(256), 0, st, slab, static_cast<uint32_t*>(d_full),
                                p->width, p->height, band, (uint32_t)c->nranks, cap);
             HIPCHK(c, hipGetLastError());
         }
+        HIPCHK(c, hipEventRecord(c->ev_gath[slot], st));
+        ++c->gather_frames;
     } else {
         // Pipelined: frame k renders into slab k % kSlabs on `st` (frames may come on different
-        // streams and overlap); its gather + de-interleave run on the comm stream, in frame order,
-        // once the render's event fires.  The render of frame k + kSlabs (same slab) first waits
-        // for frame k's gather.  Waiting on a never-recorded event is a no-op.
-        if (!c->cstream) {
-            HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-            for (int i = 0; i < rrte_ctx::kSlabs; ++i) {
-                HIPCHK(c, hipEventCreateWithFlags(&c->ev_rend[i], hipEventDisableTiming));
-                HIPCHK(c, hipEventCreateWithFlags(&c->ev_gath[i], hipEventDisableTiming));
-            }
-        }
-        const int slot = (int)(c->gather_frames % rrte_ctx::kSlabs);
-        if (c->cap_slab[slot] < slice * (size_t)c->nranks) HIPCHK(c, hipStreamSynchronize(c->cstream));
-        if ((r = ensure(c, c->d_slab[slot], c->cap_slab[slot], slice * (size_t)c->nranks)) != RRTE_OK) return r;
-        uint32_t* slab = c->d_slab[slot];
-        uint32_t* mine = slab + (size_t)c->rank * slice;
-        HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[slot], 0));
+        // streams and overlap); its gather + de-interleave run on comm stream k % ncomms with that
+        // communicator once the render's event fires -- one stream per communicator, so each
+        // communicator's gathers run in issue order on every rank.  The render of frame
+        // k + kSlabs (same slab) first waits for frame k's gather.  Waiting on a never-recorded
+        // event is a no-op.
+        const int lane = (int)(c->gather_frames % (uint64_t)c->ncomms);
+        ncclComm_t gc = c->gcomm[lane] ? c->gcomm[lane] : c->comm;
+        hipStream_t gs = c->gstream[lane];
         if ((r = launch(c, s, &pp, rows, mine, nullptr, st)) != RRTE_OK) return r;
         HIPCHK(c, hipEventRecord(c->ev_rend[slot], st));
-        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_rend[slot], 0));
-        NCCLCHK(c, ncclGather(mine, slab, slice * 4, ncclUint8, root, c->comm, c->cstream));
+        HIPCHK(c, hipStreamWaitEvent(gs, c->ev_rend[slot], 0));
+        NCCLCHK(c, ncclGather(mine, slab, slice * 4, ncclUint8, root, gc, gs));
         if (c->rank == root) {
-            hipLaunchKernelGGL(deinterleave_kernel, dg, dim3(256), 0, c->cstream, slab, static_cast<uint32_t*>(d_full),
+            // frames may finish out of order across the two comm streams: the de-interleave of frame k
+            // into d_full must not overtake frame k-1's (same output buffer when the caller reuses it)
+            if (c->gather_frames > 0)
+                HIPCHK(c, hipStreamWaitEvent(gs, c->ev_gath[(c->gather_frames - 1) % rrte_ctx::kSlabs], 0));
+            hipLaunchKernelGGL(deinterleave_kernel, dg, dim3(256), 0, gs, slab, static_cast<uint32_t*>(d_full),
                                p->width, p->height, band, (uint32_t)c->nranks, cap);
             HIPCHK(c, hipGetLastError());
         }
-        HIPCHK(c, hipEventRecord(c->ev_gath[slot], c->cstream));
+        HIPCHK(c, hipEventRecord(c->ev_gath[slot], gs));
         ++c->gather_frames;
     }
     c->pending_primary = (uint64_t)p->width * rows * p->samples_per_pixel;

@@ -25,13 +25,15 @@ def _frames(n, w=320, h=200):
     return out
 
 
+@pytest.mark.parametrize("comms", ["1", "2"])
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
-def test_gather_path_matches_plain_render(overlap, jit, monkeypatch):
+def test_gather_path_matches_plain_render(overlap, jit, comms, monkeypatch):
     import torch
 
     monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
-    frames = _frames(5)
+    monkeypatch.setenv("RRTE_GATHER_COMMS", comms)
+    frames = _frames(7)
     w, h = frames[0][1].width, frames[0][1].height
     ref = Context(0, jit=jit)
     want = []
@@ -47,14 +49,14 @@ def test_gather_path_matches_plain_render(overlap, jit, monkeypatch):
     ctx.check(lib.rrte_hip_comm_unique_id(uid))
     ctx.check(lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
     dev = torch.device("cuda", 0)
-    stream = torch.cuda.Stream(dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]  # frames in flight, as bench.py runs them
     outs = [torch.empty(w * h, dtype=torch.int32, device=dev) for _ in frames]
-    for (sc, prm), o in zip(frames, outs):
+    for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
         p = abi.RenderParams.from_buffer_copy(prm)
         if overlap:
             p.flags |= abi.FLAG_GATHER_OVERLAP
         ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(p), 0, o.data_ptr(),
-                                                    C.c_void_p(stream.cuda_stream)))
+                                                    C.c_void_p(streams[i % 3].cuda_stream)))
     ctx.check(lib.rrte_hip_synchronize(ctx.h))
     for i, o in enumerate(outs):
         got = o.cpu().numpy().view(np.uint8)
