@@ -165,6 +165,9 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # rehearsal on a box with fewer GPUs than ranks: RRTE_BENCH_DEVICE pins every rank to one device
+    if os.environ.get("RRTE_BENCH_DEVICE") is not None:
+        local_rank = int(os.environ["RRTE_BENCH_DEVICE"])
     dist_on = world > 1
     if dist_on:
         dist.init_process_group("gloo")  # control plane only; the frame gather is RCCL inside librrte_hip
