@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--mode", default="lambert_shadow", choices=["lambert_shadow", "refcompat"])
     ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--spp", type=int, default=None, help="override samples per pixel (profiling other configs)")
+    ap.add_argument("--max-depth", type=int, default=None, help="override max_depth")
+    ap.add_argument("--random", action="store_true", help="random jitter (and scatter) instead of pixel centres")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stock", action="store_true", help="skip the stock-config secondary measurement")
@@ -176,6 +179,12 @@ def main():
 
     objs, lights, cam, cfg = scenes.SCENES[args.scene](args.width, args.height, mode=args.mode)
     cfg.band_rows = args.band_rows
+    if args.spp is not None:
+        cfg.samples_per_pixel = args.spp
+    if args.max_depth is not None:
+        cfg.max_depth = args.max_depth
+    if args.random:
+        cfg.jitter = "random"
     scene = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
     if world > 1 and not args.no_overlap:
@@ -313,7 +322,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.scene} {W}x{H}, {args.mode}, spp=1, pixel-centre jitter"
+                "workload": f"{args.scene} {W}x{H}, {args.mode}, spp={prm.samples_per_pixel}, max_depth={prm.max_depth}, "
+                            + ("random jitter" if args.random else "pixel-centre jitter")
                             + (f", {args.band_rows}-row bands interleaved over {world} GPUs + RCCL gather to rank 0"
                                + (" (on the render stream)" if args.no_overlap else
                                   " pipelined against the next frame's render")
