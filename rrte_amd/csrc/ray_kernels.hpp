@@ -1097,59 +1097,88 @@ __device__ __forceinline__ const DMaterial* material_of(const S& sc, int idx) {
 // ambient + sum(light.color*I*att) + albedo * ray_color(scatter).  The
 // reference recursion color_d = local_d + albedo_d * color_{d+1} is evaluated
 // forward with a running albedo product: bit-identical to the recursion for
-// max_depth <= 2 (the parity configs use 1), rounding-level beyond.
-// SINGLE (scene-specialised kernels): one bounce only (max_depth == 1).
+// max_depth <= 2 (the parity configs use 1), rounding-level beyond.  A path is
+// advanced one bounce at a time (path_step) so that the kernel can start a
+// lane's next sample as soon as its current path ends (see ray_kernel_body).
+struct PathState {
+    Ray r;
+    Col out;
+    float tr, tg, tb;  // running albedo product
+    uint32_t depth;
+};
+
+__device__ __forceinline__ void path_begin(PathState& ps, const Ray& r) {
+    ps.r = r;
+    ps.out = Col{0.0f, 0.0f, 0.0f, 1.0f};
+    ps.tr = ps.tg = ps.tb = 1.0f;
+    ps.depth = 0;
+}
+
+// One bounce of ray_color (kp.max_depth >= 1); true when the path has ended.
+template <class S>
+__device__ __forceinline__ bool path_step(const S& sc, const KParams& kp, PathState& ps, uint32_t& st) {
+    Hit h;
+    const int idx = closest_hit(sc, ps.r, kp.t_min, h);
+    const uint32_t depth = ps.depth;
+    if (idx < 0) {
+        if (depth == 0) {
+            ps.out = Col{kp.bg[0], kp.bg[1], kp.bg[2], kp.bg[3]};
+        } else {
+            ps.out.r = ps.out.r + ps.tr * kp.bg[0];
+            ps.out.g = ps.out.g + ps.tg * kp.bg[1];
+            ps.out.b = ps.out.b + ps.tb * kp.bg[2];
+        }
+        return true;
+    }
+    const DMaterial* m = material_of(sc, idx);
+    if (!m) return true;  // BLACK
+    float ar = m->albedo[0], ag = m->albedo[1], ab = m->albedo[2], aa = m->albedo[3];
+    // BLACK + ambient_color()*0.1 (raytracer.rs:124, material.rs:10-12)
+    float cr = 0.0f + (ar * 0.1f) * 0.1f;
+    float cg = 0.0f + (ag * 0.1f) * 0.1f;
+    float cb = 0.0f + (ab * 0.1f) * 0.1f;
+    float ca = 1.0f + (aa * 0.1f) * 0.1f;
+    for_each_light(sc, [&](auto lii) {
+        Contrib k = illuminate(light_at(sc, lii), h.p);
+        cr = cr + k.cr * k.att;
+        cg = cg + k.cg * k.att;
+        cb = cb + k.cb * k.att;
+        ca = ca + k.ca * k.att;
+    });
+    if (depth == 0) {
+        ps.out = Col{cr, cg, cb, ca};
+    } else {
+        ps.out.r = ps.out.r + ps.tr * cr;
+        ps.out.g = ps.out.g + ps.tg * cg;
+        ps.out.b = ps.out.b + ps.tb * cb;
+    }
+    Ray sc_ray;
+    if (!scatter(*m, ps.r, h, st, sc_ray)) return true;
+    if (depth == 0) ps.out.a = ps.out.a + 1.0f;  // Color::from(Vec3) has alpha 1 (color.rs:78-82)
+    if (depth + 1 >= kp.max_depth) return true;   // ray_color(depth 0) == BLACK: adds 0
+    ps.tr = ps.tr * ar;
+    ps.tg = ps.tg * ag;
+    ps.tb = ps.tb * ab;
+    ps.r = sc_ray;
+    ps.depth = depth + 1;
+    return false;
+}
+
+// The whole path of one camera ray.  SINGLE (scene-specialised straight-line kernels): one
+// bounce only (max_depth <= 1).
 template <class S, bool SINGLE>
 __device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray r, uint32_t& st) {
-    Col out{0.0f, 0.0f, 0.0f, 1.0f};
-    if (kp.max_depth == 0) return out;
-    float tr = 1.0f, tg = 1.0f, tb = 1.0f;  // running albedo product
-    const uint32_t ndepth = SINGLE ? 1u : kp.max_depth;
-    for (uint32_t depth = 0; depth < ndepth; ++depth) {
-        Hit h;
-        int idx = closest_hit(sc, r, kp.t_min, h);
-        if (idx < 0) {
-            if (depth == 0) {
-                out = Col{kp.bg[0], kp.bg[1], kp.bg[2], kp.bg[3]};
-            } else {
-                out.r = out.r + tr * kp.bg[0];
-                out.g = out.g + tg * kp.bg[1];
-                out.b = out.b + tb * kp.bg[2];
-            }
-            break;
+    PathState ps;
+    path_begin(ps, r);
+    if (kp.max_depth == 0) return ps.out;
+    if constexpr (SINGLE) {
+        path_step(sc, kp, ps, st);
+    } else {
+#pragma unroll 1
+        while (!path_step(sc, kp, ps, st)) {
         }
-        const DMaterial* m = material_of(sc, idx);
-        if (!m) break;  // BLACK
-        float ar = m->albedo[0], ag = m->albedo[1], ab = m->albedo[2], aa = m->albedo[3];
-        // BLACK + ambient_color()*0.1 (raytracer.rs:124, material.rs:10-12)
-        float cr = 0.0f + (ar * 0.1f) * 0.1f;
-        float cg = 0.0f + (ag * 0.1f) * 0.1f;
-        float cb = 0.0f + (ab * 0.1f) * 0.1f;
-        float ca = 1.0f + (aa * 0.1f) * 0.1f;
-        for_each_light(sc, [&](auto lii) {
-            Contrib k = illuminate(light_at(sc, lii), h.p);
-            cr = cr + k.cr * k.att;
-            cg = cg + k.cg * k.att;
-            cb = cb + k.cb * k.att;
-            ca = ca + k.ca * k.att;
-        });
-        if (depth == 0) {
-            out = Col{cr, cg, cb, ca};
-        } else {
-            out.r = out.r + tr * cr;
-            out.g = out.g + tg * cg;
-            out.b = out.b + tb * cb;
-        }
-        Ray sc_ray;
-        if (!scatter(*m, r, h, st, sc_ray)) break;
-        if (depth == 0) out.a = out.a + 1.0f;  // Color::from(Vec3) has alpha 1 (color.rs:78-82)
-        if (depth + 1 >= kp.max_depth) break;   // ray_color(depth 0) == BLACK: adds 0
-        tr = tr * ar;
-        tg = tg * ag;
-        tb = tb * ab;
-        r = sc_ray;
     }
-    return out;
+    return ps.out;
 }
 
 // LAMBERT_SHADOW (build-defined) for one camera ray.  Called by
@@ -1263,8 +1292,9 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     uint32_t nshadow = 0;
     Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
     const uint32_t nsamples = SINGLE ? 1u : kp.spp;
-    for (uint32_t s = 0; s < nsamples; ++s) {
-        uint32_t st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
+    // camera ray of sample s (raytracer.rs:66-70): per-(pixel, sample) RNG stream, jitter, generate_ray
+    auto camera_ray = [&](uint32_t s, uint32_t& st) {
+        st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
         float jx = 0.5f, jy = 0.5f;
         if (kp.jitter == RRTE_JITTER_RANDOM) {
             jx = rng_f32(st);
@@ -1272,17 +1302,51 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
         }
         float u = ((float)xc + jx) / (float)kp.width;
         float v = ((float)y + jy) / (float)kp.height;
-        Ray r = generate_ray(kp, u, v);
-        Col c{0.0f, 0.0f, 0.0f, 1.0f};
-        if (MODE == RRTE_MODE_LAMBERT_SHADOW) {
-            c = shade_lambert<S, CULL>(sc, kp, cl, r, live, nshadow);
-        } else if (live) {
-            c = ray_color_ref<S, SINGLE>(sc, kp, r, st);
-        }
+        return generate_ray(kp, u, v);
+    };
+    auto accumulate = [&](const Col& c) {
         acc.r = acc.r + c.r;
         acc.g = acc.g + c.g;
         acc.b = acc.b + c.b;
         acc.a = acc.a + c.a;
+    };
+    if constexpr (MODE == RRTE_MODE_REFCOMPAT && !SINGLE) {
+        // Path regeneration: one loop advances every lane's current path by one bounce; a lane
+        // whose path ends adds its colour and starts its next sample at once.  A wave then costs
+        // the largest per-lane total of bounces instead of the sum over samples of each sample's
+        // longest path.  Same per-sample RNG streams and accumulation order as the nested loops.
+        if (kp.max_depth == 0) {
+            for (uint32_t s = 0; s < nsamples; ++s) accumulate(Col{0.0f, 0.0f, 0.0f, 1.0f});
+        } else {
+            uint32_t s = 0, st = 0;
+            bool active = false;
+            PathState ps;
+#pragma unroll 1
+            for (;;) {
+                if (!active && live && s < nsamples) {
+                    path_begin(ps, camera_ray(s, st));
+                    active = true;
+                }
+                if (!__any(active)) break;
+                if (active && path_step(sc, kp, ps, st)) {
+                    accumulate(ps.out);
+                    active = false;
+                    ++s;
+                }
+            }
+        }
+    } else {
+        for (uint32_t s = 0; s < nsamples; ++s) {
+            uint32_t st;
+            Ray r = camera_ray(s, st);
+            Col c{0.0f, 0.0f, 0.0f, 1.0f};
+            if (MODE == RRTE_MODE_LAMBERT_SHADOW) {
+                c = shade_lambert<S, CULL>(sc, kp, cl, r, live, nshadow);
+            } else if (live) {
+                c = ray_color_ref<S, SINGLE>(sc, kp, r, st);
+            }
+            accumulate(c);
+        }
     }
     if (live) {
         acc.r = acc.r * kp.inv_spp;
