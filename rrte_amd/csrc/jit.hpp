@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <vector>
 
 #include "device_scene.hpp"
 
@@ -21,6 +22,18 @@ struct JitKernel {
 // (single: one sample, one bounce -> straight-line code; else runtime sample/bounce loops).
 std::string jit_source(const DPrim* prims, uint32_t np, const DMaterial* mats, uint32_t nm, const DLight* lights,
                        uint32_t nl, const rrte_sdf_node* nodes, uint32_t nn, int mode, bool cull, bool single);
+
+// A compiled code object (hiprtc only: no device API, safe on a background thread).
+struct JitCode {
+    bool ok = false;
+    std::vector<char> code;
+    std::string log;
+    double compile_ms = 0.0;
+};
+JitCode jit_compile_code(const std::string& src);  // compiles are serialised internally
+
+// Load a compiled code object on the current device.
+bool jit_load(const JitCode& jc, JitKernel& out, std::string& log);
 
 // hiprtc compile for gfx950 + module load.  On failure `log` holds the reason.
 bool jit_compile(const std::string& src, JitKernel& out, std::string& log);

@@ -15,6 +15,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <future>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -87,6 +88,7 @@ struct rrte_ctx {
     std::vector<DLight> h_lights;
     std::vector<rrte_sdf_node> h_nodes;
     std::unordered_map<std::string, JitKernel> jit_cache;  // failed compiles cached with fn == nullptr
+    std::unordered_map<std::string, std::future<JitCode>> jit_pending;  // AUTO: background compiles
     std::string jit_log;
 };
 
@@ -547,22 +549,41 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
     };
     auto it = c->jit_cache.find(key);
     if (it != c->jit_cache.end()) return remember(it->second.fn ? &it->second : nullptr);
-    if (!(c->jit_mode == RRTE_JIT_ON || c->same_scene_renders >= 1)) return nullptr;
-    if (c->jit_cache.size() >= 32) {
-        for (auto& kv : c->jit_cache) jit_release(kv.second);
-        c->jit_cache.clear();
-        last.valid = false;
-    }
-    std::string src = jit_source(c->h_prims.data(), (uint32_t)c->h_prims.size(), c->h_mats.data(),
-                                 (uint32_t)c->h_mats.size(), c->h_lights.data(), (uint32_t)c->h_lights.size(),
-                                 c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull, single);
     JitKernel jk;
     std::string log;
-    if (hipSetDevice(c->device) != hipSuccess || !jit_compile(src, jk, log)) {
-        c->jit_log = log;  // stay on the generic kernel for this scene
-        jk = JitKernel{};
+    auto pend = c->jit_pending.find(key);
+    if (pend != c->jit_pending.end()) {
+        // AUTO: a background compile of this scene is running; keep the generic kernel until it lands
+        if (pend->second.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return nullptr;
+        const JitCode jc = pend->second.get();
+        c->jit_pending.erase(pend);
+        if (hipSetDevice(c->device) != hipSuccess || !jit_load(jc, jk, log)) {
+            c->jit_log = log;
+            jk = JitKernel{};
+        } else {
+            c->stats.jit_compile_ms = jk.compile_ms;
+        }
     } else {
-        c->stats.jit_compile_ms = jk.compile_ms;
+        if (!(c->jit_mode == RRTE_JIT_ON || c->same_scene_renders >= 1)) return nullptr;
+        if (c->jit_cache.size() >= 32) {
+            for (auto& kv : c->jit_cache) jit_release(kv.second);
+            c->jit_cache.clear();
+            last.valid = false;
+        }
+        std::string src = jit_source(c->h_prims.data(), (uint32_t)c->h_prims.size(), c->h_mats.data(),
+                                     (uint32_t)c->h_mats.size(), c->h_lights.data(), (uint32_t)c->h_lights.size(),
+                                     c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull, single);
+        if (c->jit_mode == RRTE_JIT_AUTO) {
+            // compile on a background thread (hiprtc only); frames keep running on the generic kernel
+            c->jit_pending.emplace(key, std::async(std::launch::async, [src]() { return jit_compile_code(src); }));
+            return nullptr;
+        }
+        if (hipSetDevice(c->device) != hipSuccess || !jit_compile(src, jk, log)) {
+            c->jit_log = log;  // stay on the generic kernel for this scene
+            jk = JitKernel{};
+        } else {
+            c->stats.jit_compile_ms = jk.compile_ms;
+        }
     }
     auto& slot = c->jit_cache[key];
     slot = jk;
@@ -696,9 +717,10 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
 void rrte_hip_destroy(rrte_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();  // frames may still run on caller streams
     if (c->gcomm[1] && c->gcomm[1] != c->comm) ncclCommDestroy(c->gcomm[1]);
     if (c->comm) ncclCommDestroy(c->comm);
+    c->jit_pending.clear();  // joins background compiles
     for (auto& kv : c->jit_cache) jit_release(kv.second);
     for (hipStream_t gs : c->gstream)
         if (gs) (void)hipStreamSynchronize(gs);

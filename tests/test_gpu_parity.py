@@ -163,15 +163,24 @@ def test_empty_scene_no_lights_depth0_and_no_material():
     compare(objs, lights, cam, cfg)
 
 
-def test_jit_auto_policy_specialises_on_second_frame():
+def test_jit_auto_policy_specialises_in_the_background():
+    """AUTO (the default): the second render of an unchanged scene starts a background compile;
+    frames keep running on the generic kernel until the specialised one is loaded, and every frame is
+    identical whichever kernel rendered it."""
+    import time
     objs, lights, cam, cfg = scenes.sdf_showcase(96, 54)
     rt = Raytracer(cfg, device=0, jit=abi.JIT_AUTO)
     a = rt.render(objs, lights, [], cam)
     assert rt.stats().jit_active == 0
-    b = rt.render(objs, lights, [], cam)
-    st = rt.stats()
-    assert st.jit_active == 1 and st.jit_compile_ms > 0
-    assert np.array_equal(a, b)
+    t0, frames = time.time(), 1
+    while True:
+        b = rt.render(objs, lights, [], cam)
+        frames += 1
+        assert np.array_equal(a, b)
+        if rt.stats().jit_active:
+            break
+        assert time.time() - t0 < 120, "the background compile never landed"
+    assert frames >= 3 and rt.stats().jit_compile_ms > 0  # frame 2 only started the compile
     cam.transform.position = (cam.transform.position[0], cam.transform.position[1] + np.float32(0.5),
                               cam.transform.position[2])
     c = rt.render(objs, lights, [], cam)  # camera motion: no recompile, still specialised
