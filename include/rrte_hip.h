@@ -310,6 +310,18 @@ rrte_status rrte_hip_set_jit(rrte_ctx* ctx, int mode);
 /* Diagnostic: generate + hiprtc-compile the specialised kernel for `scene`
  * (no device needed).  RRTE_OK if it compiles; otherwise the log is copied out. */
 rrte_status rrte_hip_jit_check(const rrte_scene_ir* scene, int mode, char* log, size_t log_len);
+/* Diagnostic: run the kernels' short correctly rounded f32 sequences (device_scene.hpp
+ * sqrt_rn / rcp_rn / the constant-divisor step of div_rn) on `device` against the
+ * compiler's full sequences and count bit mismatches (any NaN matches any NaN):
+ *   RRTE_FPCHECK_SQRT, RRTE_FPCHECK_RCP: every f32 bit pattern in [lo, hi) (hi <= 2^32);
+ *   RRTE_FPCHECK_DIV: a/b for every significand of a in [1, 2) and every b = 1 + k*2^-23,
+ *                     k in [lo, hi) (hi <= 2^23), with y = rcp_rn(b).  Synchronous. */
+/*   RRTE_FPCHECK_SQRT_HW: control -- the bare v_sqrt_f32 against the correctly rounded sqrt
+ *                         (the sweep must find its 1-ulp errors). */
+typedef enum rrte_fpcheck {
+    RRTE_FPCHECK_SQRT = 0, RRTE_FPCHECK_RCP = 1, RRTE_FPCHECK_DIV = 2, RRTE_FPCHECK_SQRT_HW = 3
+} rrte_fpcheck;
+rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uint64_t* mismatches);
 
 /* ----------------------------------------------------- multi-GPU (RCCL/xGMI) */
 /* Row-band partition: band b (band_rows rows) belongs to rank b % nranks.

@@ -35,6 +35,7 @@ SDF_POP_POINT = 96
 SDF_MAX_STACK, SDF_MAX_POINT_STACK, SDF_MAX_OCTAVES = 8, 4, 8
 UNIQUE_ID_BYTES = 128
 JIT_OFF, JIT_ON, JIT_AUTO = 0, 1, 2
+FPCHECK_SQRT, FPCHECK_RCP, FPCHECK_DIV, FPCHECK_SQRT_HW = 0, 1, 2, 3
 
 
 # --------------------------------------------------------------- structs
@@ -121,6 +122,7 @@ EXPORTS = {
     "rrte_hip_stats": (C.c_int, [_P, C.POINTER(Stats)]),
     "rrte_hip_set_jit": (C.c_int, [_P, C.c_int]),
     "rrte_hip_jit_check": (C.c_int, [C.POINTER(SceneIR), C.c_int, C.c_char_p, C.c_size_t]),
+    "rrte_hip_fpcheck": (C.c_int, [C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "rrte_hip_comm_unique_id": (C.c_int, [_P]),
     "rrte_hip_comm_init": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "rrte_hip_render_gather": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_int, _P]),

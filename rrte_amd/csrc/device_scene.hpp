@@ -82,17 +82,67 @@ struct KParams {
 struct f3 { float x, y, z; };
 
 __device__ __forceinline__ f3 V(float x, float y, float z) { return f3{x, y, z}; }
+// Correctly rounded f32 sqrt (Rust f32::sqrt), 11 VALU ops instead of the compiler's 16.
+// v_sqrt_f32 is within 1 ulp; the neighbour whose residual x - s*(s -/+ ulp) changes sign
+// is taken (two fmas).  That is exact for every input except magnitudes in (0, 2^-96),
+// where the residuals underflow: those lanes (a divergent branch no real scene takes)
+// recompute with the compiler's scaled sequence.  Verified bit-identical to __builtin_sqrtf
+// over all 2^32 inputs on gfx950 (rrte_hip_fpcheck, tests/test_gpu_fpexact.py).
+// RRTE_ABLATE_FAST_SQRT swaps in the bare 1-ulp v_sqrt_f32 -- a timing experiment only
+// (breaks parity), never a build setting.
+#ifdef RRTE_ABLATE_FAST_SQRT
+__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_amdgcn_sqrtf(x); }
+#else
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float lo = __uint_as_float(__float_as_uint(s) - 1u), hi = __uint_as_float(__float_as_uint(s) + 1u);
+    const float elo = __builtin_fmaf(-lo, s, x), ehi = __builtin_fmaf(-hi, s, x);
+    float r = (elo <= 0.0f) ? lo : s;
+    r = (ehi > 0.0f) ? hi : r;
+    if (__builtin_expect(__builtin_fabsf(x) < 0x1.0p-96f && x != 0.0f, 0)) r = __builtin_sqrtf(x);
+    return r;
+}
+#endif
+// Correctly rounded 1/b: v_rcp_f32 and one Newton fma step is exact for every b with
+// |b| in [2^-126, 2^126] (rrte_hip_fpcheck: all 2^32 inputs on gfx950); zeros,
+// denormals, huge values, inf and NaN take the compiler's full divide.  5 VALU ops instead of 11.
+__device__ __forceinline__ float rcp_rn(float b) {
+    if (__builtin_constant_p(b)) return 1.0f / b;
+    float y = __builtin_amdgcn_rcpf(b);
+    y = __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
+    if (__builtin_expect(!(__builtin_fabsf(b) >= 0x1.0p-126f && __builtin_fabsf(b) <= 0x1.0p+126f), 0)) y = 1.0f / b;
+    return y;
+}
+// Correctly rounded a/b.  When b folds to a constant (scene-specialised kernels: SDF and
+// primitive parameters), y = RN(1/b) is a constant and q = RN(a*y), r = a - b*q (exact fma),
+// RN(q + r*y) is the correctly rounded quotient for every a with |a| in [2^-60, 2^60] and
+// |b| in [2^-60, 2^60] (Markstein; checked over all 2^46 significand pairs on gfx950,
+// rrte_hip_fpcheck -- the steps are correctly rounded, so the result is
+// exponent-invariant inside that range).  Other a take the full divide.  Runtime divisors
+// keep the compiler's sequence (a guarded short form would not be shorter).
+__device__ __forceinline__ float div_by_rcp(float a, float b, float y) {  // y = RN(1/b)
+    const float q = a * y;
+    return __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
+}
+__device__ __forceinline__ float div_rn(float a, float b) {
+    if (__builtin_constant_p(b) && __builtin_fabsf(b) >= 0x1.0p-60f && __builtin_fabsf(b) <= 0x1.0p+60f) {
+        float r = div_by_rcp(a, b, 1.0f / b);
+        if (__builtin_expect(!(__builtin_fabsf(a) >= 0x1.0p-60f && __builtin_fabsf(a) <= 0x1.0p+60f), 0)) r = a / b;
+        return r;
+    }
+    return a / b;
+}
 __device__ __forceinline__ f3 vadd(f3 a, f3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ f3 vsub(f3 a, f3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ f3 vneg(f3 a) { return V(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ f3 vmuls(f3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ f3 vdivs(f3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ f3 vdivs(f3 a, float s) { return V(div_rn(a.x, s), div_rn(a.y, s), div_rn(a.z, s)); }
 // glam Vec3::dot, left to right
 __device__ __forceinline__ float vdot(f3 a, f3 b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
 __device__ __forceinline__ float vlen2(f3 a) { return vdot(a, a); }
-__device__ __forceinline__ float vlen(f3 a) { return __builtin_sqrtf(vdot(a, a)); }
+__device__ __forceinline__ float vlen(f3 a) { return sqrt_rn(vdot(a, a)); }
 // glam Vec3::normalize: self * (1 / length())
-__device__ __forceinline__ f3 vnorm(f3 a) { return vmuls(a, 1.0f / __builtin_sqrtf(vdot(a, a))); }
+__device__ __forceinline__ f3 vnorm(f3 a) { return vmuls(a, rcp_rn(sqrt_rn(vdot(a, a)))); }
 __device__ __forceinline__ f3 vcross(f3 a, f3 b) {
     return V(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
 }

@@ -98,8 +98,8 @@ __device__ __forceinline__ void for_each_light(const S& sc, F&& f) {
 }
 
 // ------------------------------------------------------------- SDF program
-__device__ __forceinline__ float len2f(float a, float b) { return __builtin_sqrtf(a * a + b * b); }
-__device__ __forceinline__ float len3f(float a, float b, float c) { return __builtin_sqrtf((a * a + b * b) + c * c); }
+__device__ __forceinline__ float len2f(float a, float b) { return sqrt_rn(a * a + b * b); }
+__device__ __forceinline__ float len3f(float a, float b, float c) { return sqrt_rn((a * a + b * b) + c * c); }
 
 __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__ f, f3 p) {
     f3 q = vsub(p, V(f[0], f[1], f[2]));
@@ -143,12 +143,12 @@ __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__
         float k1mqx = 0.0f - qx, k1mqy = hh - qy;
         float tnum = k1mqx * k2x + k1mqy * k2y;
         float tden = k2x * k2x + k2y * k2y;
-        float t = clampf_(tnum / tden, 0.0f, 1.0f);
+        float t = clampf_(div_rn(tnum, tden), 0.0f, 1.0f);
         float cbx = (qx - 0.0f) + k2x * t;
         float cby = (qy - hh) + k2y * t;
         float s = (cbx < 0.0f && cay < 0.0f) ? -1.0f : 1.0f;
         float da = cax * cax + cay * cay, db = cbx * cbx + cby * cby;
-        return s * __builtin_sqrtf(mn(da, db));
+        return s * sqrt_rn(mn(da, db));
     }
     case RRTE_SDF_CAPSULE: {
         float hh = f[4] * 0.5f;
@@ -157,8 +157,8 @@ __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__
     }
     case RRTE_SDF_ELLIPSOID: {
         float rx = f[4], ry = f[5], rz = f[6];
-        float k0 = len3f(q.x / rx, q.y / ry, q.z / rz);
-        float k1 = len3f(q.x / (rx * rx), q.y / (ry * ry), q.z / (rz * rz));
+        float k0 = len3f(div_rn(q.x, rx), div_rn(q.y, ry), div_rn(q.z, rz));
+        float k1 = len3f(div_rn(q.x, rx * rx), div_rn(q.y, ry * ry), div_rn(q.z, rz * rz));
         if (!(k1 > 0.0f)) return -mn(rx, mn(ry, rz));
         return k0 * (k0 - 1.0f) / k1;
     }
@@ -169,7 +169,7 @@ __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__
 
 // smooth_min (README.md:485-488)
 __device__ __forceinline__ float smin(float a, float b, float k) {
-    float h = clampf_(0.5f + (0.5f * (b - a)) / k, 0.0f, 1.0f);
+    float h = clampf_(0.5f + div_rn(0.5f * (b - a), k), 0.0f, 1.0f);
     float om = 1.0f - h;
     return (a * h + b * om) - (k * h) * om;
 }
@@ -194,7 +194,7 @@ __device__ __forceinline__ f3 sdf_deform(uint32_t op, const uint32_t* __restrict
     case RRTE_SDF_TAPER: {
         uint32_t ax = iarg[0];
         uint32_t u = (ax + 1) % 3, w = (ax + 2) % 3;
-        float t = clampf_((comp(q, ax) + f[5] * 0.5f) / f[5], 0.0f, 1.0f);
+        float t = clampf_(div_rn(comp(q, ax) + f[5] * 0.5f, f[5]), 0.0f, 1.0f);
         float s = f[3] + (f[4] - f[3]) * t;
         q = setcomp(q, u, comp(q, u) / s);
         q = setcomp(q, w, comp(q, w) / s);
@@ -312,7 +312,7 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     float cc = vdot(oc, oc) - br * br;
     float disc = b * b - cc;
     if (disc < 0.0f) return false;
-    float sq = __builtin_sqrtf(disc);
+    float sq = sqrt_rn(disc);
     float t = mx(t_min, -b - sq);
     float tend = mn(t_max, -b + sq);
     if (t > tend) return false;
@@ -375,7 +375,7 @@ __device__ __forceinline__ bool isect_sphere(const DPrim& pr, const Ray& r, floa
     float cc = vlen2(oc) - rad * rad;
     float disc = hb * hb - a * cc;
     if (disc < 0.0f) return false;
-    float sq = __builtin_sqrtf(disc);
+    float sq = sqrt_rn(disc);
     float root = (-hb - sq) / a;
     if (root < t_min || t_max < root) {
         root = (-hb + sq) / a;
@@ -405,7 +405,7 @@ __device__ __forceinline__ bool isect_triangle(const DPrim& pr, const Ray& r, fl
     f3 h = vcross(r.d, e2);
     float a = vdot(e1, h);
     if (a > -1e-6f && a < 1e-6f) return false;
-    float f = 1.0f / a;
+    float f = rcp_rn(a);
     f3 s = vsub(r.o, v0);
     float u = f * vdot(s, h);
     if (u < 0.0f || u > 1.0f) return false;
@@ -469,7 +469,7 @@ __device__ __forceinline__ bool isect_cylinder(const DPrim& pr, const Ray& r, fl
     float cc = oc.x * oc.x + oc.z * oc.z - rad * rad;
     float disc = b * b - 4.0f * a * cc;
     if (disc < 0.0f) return false;
-    float sq = __builtin_sqrtf(disc);
+    float sq = sqrt_rn(disc);
     float ts0 = (-b - sq) / (2.0f * a), ts1 = (-b + sq) / (2.0f * a);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -500,7 +500,7 @@ __device__ __forceinline__ bool isect_cone(const DPrim& pr, const Ray& r, float 
     float cc = oc.x * oc.x + oc.z * oc.z - k2 * (oc.y - hh) * (oc.y - hh);
     float disc = b * b - 4.0f * a * cc;
     if (disc < 0.0f) return false;
-    float sq = __builtin_sqrtf(disc);
+    float sq = sqrt_rn(disc);
     float ts0 = (-b - sq) / (2.0f * a), ts1 = (-b + sq) / (2.0f * a);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -509,7 +509,7 @@ __device__ __forceinline__ bool isect_cone(const DPrim& pr, const Ray& r, float 
             f3 p = ray_at(lr, t);
             float yl = p.y - ctr.y;
             if (yl >= -hh && yl <= hh) {
-                float rr = __builtin_sqrtf(p.x * p.x + p.z * p.z);
+                float rr = sqrt_rn(p.x * p.x + p.z * p.z);
                 f3 ln = vnorm(V(p.x / rr, k, p.z / rr));
                 hit_new(out, t, m_point(pr.xf, p), vnorm(m_vector(pr.xf, ln)), r);
                 return true;
@@ -536,7 +536,7 @@ __device__ __forceinline__ bool isect_capsule(const DPrim& pr, const Ray& r, flo
         float cc = vlen2(oc) - rad * rad;
         float disc = hb * hb - a * cc;
         if (disc >= 0.0f) {
-            float sq = __builtin_sqrtf(disc);
+            float sq = sqrt_rn(disc);
             float ts0 = (-hb - sq) / a, ts1 = (-hb + sq) / a;
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -560,7 +560,7 @@ __device__ __forceinline__ bool isect_capsule(const DPrim& pr, const Ray& r, flo
     float ccy = oc.x * oc.x + oc.z * oc.z - rad * rad;
     float disc = bc * bc - 4.0f * ac * ccy;
     if (disc >= 0.0f) {
-        float sq = __builtin_sqrtf(disc);
+        float sq = sqrt_rn(disc);
         float ts0 = (-bc - sq) / (2.0f * ac), ts1 = (-bc + sq) / (2.0f * ac);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -597,7 +597,7 @@ __device__ __forceinline__ bool mt_test(f3 v0, f3 e1, f3 e2, const Ray& r, float
     f3 h = vcross(r.d, e2);
     float a = vdot(e1, h);
     if (a > -1e-6f && a < 1e-6f) return false;
-    float f = 1.0f / a;
+    float f = rcp_rn(a);
     f3 s = vsub(r.o, v0);
     u = f * vdot(s, h);
     if (u < 0.0f || u > 1.0f) return false;
@@ -670,7 +670,7 @@ __device__ __forceinline__ bool isect_mesh(const DPrim& pr, const MeshView& mv, 
             }
         }
     } else {
-        const f3 inv = V(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+        const f3 inv = V(rcp_rn(r.d.x), rcp_rn(r.d.y), rcp_rn(r.d.z));
         uint32_t* stk = mesh_stack();
         int sp = 0;
         uint32_t link = count ? pr.sdf_first : 0u;
@@ -910,7 +910,7 @@ __device__ __forceinline__ HitBound wave_hit_bound(bool hit, f3 p, f3 n, float b
     b.unsafe = __any(hit && !use);
     b.c = V((lx + hx) * 0.5f, (ly + hy) * 0.5f, (lz + hz) * 0.5f);
     f3 d = V(hx - lx, hy - ly, hz - lz);
-    b.r = 0.5f * __builtin_sqrtf(vdot(d, d));
+    b.r = 0.5f * sqrt_rn(vdot(d, d));
     b.ext = wave_max(use ? ext : 0.0f);
     return b;
 }
@@ -957,7 +957,7 @@ struct Contrib { float cr, cg, cb, ca; f3 dir; float dist, att; };
 // PointLight::calculate_attenuation (light.rs:170-178)
 __device__ __forceinline__ float point_att(const DLight& l, float d) {
     if (d > l.range) return 0.0f;
-    float a = 1.0f / ((1.0f + l.linear * d) + (l.quadratic * d) * d);
+    float a = rcp_rn((1.0f + l.linear * d) + (l.quadratic * d) * d);
     return mx(a, 0.0f);
 }
 
@@ -1030,10 +1030,10 @@ __device__ __forceinline__ bool scatter(const DMaterial& m, const Ray& rin, cons
         return false;
     }
     case RRTE_MAT_DIELECTRIC: {
-        float ratio = h.front ? 1.0f / m.ior : m.ior;
+        float ratio = h.front ? rcp_rn(m.ior) : m.ior;
         f3 ud = vnorm(rin.d);
         float cos_t = mn(vdot(vneg(ud), h.n), 1.0f);
-        float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+        float sin_t = sqrt_rn(1.0f - cos_t * cos_t);
         bool cannot = ratio * sin_t > 1.0f;
         float r0 = (1.0f - ratio) / (1.0f + ratio);
         r0 = r0 * r0;
@@ -1049,7 +1049,7 @@ __device__ __forceinline__ bool scatter(const DMaterial& m, const Ray& rin, cons
             float ct = mn(vdot(vneg(ud), h.n), 1.0f);
             f3 perp = vmuls(vadd(ud, vmuls(h.n, ct)), ratio);
             float l2 = vlen2(perp);
-            f3 par = vmuls(h.n, -__builtin_sqrtf(fabsf(1.0f - l2)));
+            f3 par = vmuls(h.n, -sqrt_rn(fabsf(1.0f - l2)));
             dir = (l2 < 1.0f) ? vadd(perp, par) : reflect3(ud, h.n);
         }
         out = ray_new(h.p, dir);

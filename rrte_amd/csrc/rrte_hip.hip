@@ -671,6 +671,39 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
 
 }  // namespace
 
+// ---------------------------------------------------------- rrte_hip_fpcheck
+// Bit-exactness sweeps of device_scene.hpp's short correctly rounded sequences against the
+// compiler's full ones.  A mismatch count is accumulated per wave (ballot + popcount).
+__device__ __forceinline__ bool fp_same(float a, float b) {
+    return (a != a && b != b) || __float_as_uint(a) == __float_as_uint(b);
+}
+__device__ __forceinline__ void fp_count(bool bad, unsigned long long* out) {
+    const unsigned long long m = __ballot(bad);
+    if (m && (threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)__popcll(m));
+}
+__global__ __launch_bounds__(256) void fpcheck_unary_kernel(int kind, uint64_t x0, uint64_t n,
+                                                            unsigned long long* out) {
+    // thread t of the launch checks patterns x0 + t + k * (launch threads), k < 64
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < stride * 64; i += stride) {
+        const bool in = i < n;
+        const float x = __uint_as_float((uint32_t)(x0 + (in ? i : 0)));
+        bool bad;
+        if (kind == RRTE_FPCHECK_SQRT) bad = !fp_same(sqrt_rn(x), __builtin_sqrtf(x));
+        else if (kind == RRTE_FPCHECK_RCP) bad = !fp_same(rcp_rn(x), 1.0f / x);
+        else bad = !fp_same(__builtin_amdgcn_sqrtf(x), __builtin_sqrtf(x));
+        fp_count(in && bad, out);
+    }
+}
+__global__ __launch_bounds__(256) void fpcheck_div_kernel(uint32_t b0, unsigned long long* out) {
+    const float b = __uint_as_float(0x3f800000u | (b0 + blockIdx.x));
+    const float y = rcp_rn(b);
+    for (uint32_t am = threadIdx.x; am < (1u << 23); am += blockDim.x) {
+        const float a = __uint_as_float(0x3f800000u | am);
+        fp_count(!fp_same(div_by_rcp(a, b, y), a / b), out);
+    }
+}
+
 extern "C" {
 
 uint32_t rrte_hip_abi_version(void) { return RRTE_ABI_VERSION; }
@@ -826,6 +859,39 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
         snprintf(log, log_len, "%s", ok ? "" : msg.c_str());
     }
     return ok ? RRTE_OK : RRTE_HIP_ERROR;
+}
+
+rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uint64_t* mismatches) {
+    if (!mismatches || kind < RRTE_FPCHECK_SQRT || kind > RRTE_FPCHECK_SQRT_HW || lo > hi ||
+        hi > (kind == RRTE_FPCHECK_DIV ? (1ull << 23) : (1ull << 32)))
+        return RRTE_INVALID_ARG;
+    if (hipSetDevice(device) != hipSuccess) return RRTE_HIP_ERROR;
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, sizeof(unsigned long long)) != hipSuccess) return RRTE_HIP_ERROR;
+    bool ok = hipMemset(d, 0, sizeof(unsigned long long)) == hipSuccess;
+    if (kind == RRTE_FPCHECK_DIV) {
+        const uint64_t chunk = 1u << 14;  // b significands per launch (one workgroup each)
+        for (uint64_t b0 = lo; ok && b0 < hi; b0 += chunk) {
+            const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, hi - b0);
+            hipLaunchKernelGGL(fpcheck_div_kernel, dim3(n), dim3(256), 0, 0, (uint32_t)b0, d);
+            ok = hipGetLastError() == hipSuccess;
+        }
+    } else {
+        const uint64_t chunk = 1ull << 26;  // bit patterns per launch, 64 per thread
+        for (uint64_t x0 = lo; ok && x0 < hi; x0 += chunk) {
+            const uint64_t n = std::min<uint64_t>(chunk, hi - x0);
+            hipLaunchKernelGGL(fpcheck_unary_kernel, dim3((uint32_t)((n + 16383) / 16384)), dim3(256), 0, 0, kind, x0,
+                               n, d);
+            ok = hipGetLastError() == hipSuccess;
+        }
+    }
+    unsigned long long h = 0;
+    ok = ok && hipDeviceSynchronize() == hipSuccess &&
+         hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess;
+    (void)hipFree(d);
+    if (!ok) return RRTE_HIP_ERROR;
+    *mismatches = h;
+    return RRTE_OK;
 }
 
 uint32_t rrte_hip_band_rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank) {

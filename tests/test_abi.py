@@ -85,3 +85,16 @@ def test_band_partition_covers_every_row_once(H, band, n):
             b, w = divmod(lr, band)
             seen.append((b * n + r) * band + w if n > 1 else lr)
     assert sorted(seen) == list(range(H))
+
+
+def test_fpcheck_rejects_bad_ranges():
+    """Argument validation happens before any device call (runs without a GPU)."""
+    import ctypes as C
+
+    out = C.c_uint64(0)
+    lib = abi.load()
+    assert lib.rrte_hip_fpcheck(0, abi.FPCHECK_DIV, 0, (1 << 23) + 1, C.byref(out)) == 1
+    assert lib.rrte_hip_fpcheck(0, 7, 0, 1, C.byref(out)) == 1
+    assert lib.rrte_hip_fpcheck(0, -1, 0, 1, C.byref(out)) == 1
+    assert lib.rrte_hip_fpcheck(0, abi.FPCHECK_SQRT, 5, 4, C.byref(out)) == 1
+    assert lib.rrte_hip_fpcheck(0, abi.FPCHECK_SQRT, 0, 1, None) == 1
