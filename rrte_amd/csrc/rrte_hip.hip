@@ -850,9 +850,13 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
     lower_scene(s, prims, mats, lights);
     MeshData md;
     build_mesh_bvhs(s, prims.data(), md, nullptr);
+    // RRTE_JIT_CHECK_MULTI=1: the multi-sample / multi-bounce variant (as the renderer picks it for
+    // spp > 1 or max_depth > 1) instead of the straight-line one
+    const char* mv = getenv("RRTE_JIT_CHECK_MULTI");
+    const bool single = !(mv && mv[0] == '1');
     std::string src = jit_source(prims.data(), (uint32_t)prims.size(), mats.data(), (uint32_t)mats.size(),
                                  lights.data(), (uint32_t)lights.size(), s->sdf_nodes, s->num_sdf_nodes, mode,
-                                 cull_policy(s, (uint32_t)mode, env_cull_setting()), true);
+                                 cull_policy(s, (uint32_t)mode, env_cull_setting()), single);
     std::string msg;
     bool ok = jit_compile_only(src, msg);
     if (log && log_len) {
