@@ -322,6 +322,15 @@ typedef enum rrte_fpcheck {
     RRTE_FPCHECK_SQRT = 0, RRTE_FPCHECK_RCP = 1, RRTE_FPCHECK_DIV = 2, RRTE_FPCHECK_SQRT_HW = 3
 } rrte_fpcheck;
 rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uint64_t* mismatches);
+/* Diagnostic (host only): the CSG early-out decoration the renderer applies to one SDF program
+ * (DESIGN.md §5 CSG guards).  Copies in[0..count) to out with, for every guarded right operand B
+ * of a union / difference op j: out[first node of B].i[2] = j + 1 and out[j].f[4..9] = B's bound
+ * (centre xyz, radius R, slope lambda, usable range): B >= lambda (|p - centre| - R) wherever
+ * R <= |p - centre| <= f[9].  min_leaves: 1 = guard every operand, 2 = the renderer's default
+ * (operands of >= 2 leaves and single leaves of the long formulas), N = operands of >= N leaves,
+ * 0 = none.  *guards = number of guards.  The program must pass the renderer's validation. */
+rrte_status rrte_hip_sdf_guards(const rrte_sdf_node* in, uint32_t count, uint32_t min_leaves, rrte_sdf_node* out,
+                                uint32_t* guards);
 
 /* ----------------------------------------------------- multi-GPU (RCCL/xGMI) */
 /* Row-band partition: band b (band_rows rows) belongs to rank b % nranks.

@@ -264,9 +264,45 @@ __device__ __forceinline__ void sdf_node_step(const rrte_sdf_node& n, float* vs,
     }
 }
 
+// Exact CSG early-out (host analysis: sdf_guard.hip).  g = the CSG op node whose right operand B
+// starts here, a = its left operand's value (top of the value stack).  Inside the guard's range
+// |p - c| in [R, smax], B >= L = lambda (|p - c| - R) (inflated bound), and when L alone decides
+// the op its result is exactly a (union: b >= L >= a; difference: -b <= -L <= a; smooth union /
+// difference: h computed with L is 1, so h(b) is 1 by monotone rounding, and with b >= L >= 0 the
+// formula reduces to a + 0 / -(-a + 0)).  Wave-uniform: taken only when every active lane may take
+// it, so the result never depends on the guard.
+__device__ __forceinline__ bool sdf_guard(const rrte_sdf_node& g, float a, f3 p, float& r) {
+    const float dx = p.x - g.f[4], dy = p.y - g.f[5], dz = p.z - g.f[6];
+    const float s = __builtin_amdgcn_sqrtf((dx * dx + dy * dy) + dz * dz);
+    const float L = g.f[8] * (s - g.f[7]);
+    bool ok = s >= g.f[7] && s <= g.f[9];
+    switch (g.op) {
+    case RRTE_SDF_UNION:
+        ok = ok && L >= a;
+        r = a;
+        break;
+    case RRTE_SDF_DIFFERENCE:
+        ok = ok && !(-L > a);
+        r = a;
+        break;
+    case RRTE_SDF_SMOOTH_UNION:
+        ok = ok && clampf_(0.5f + div_rn(0.5f * (L - a), g.f[0]), 0.0f, 1.0f) == 1.0f;
+        r = a + 0.0f;
+        break;
+    default: {  // RRTE_SDF_SMOOTH_DIFFERENCE: -smin(-a, b, k)
+        const float na = -a;
+        ok = ok && clampf_(0.5f + div_rn(0.5f * (L - na), g.f[0]), 0.0f, 1.0f) == 1.0f;
+        r = -(na + 0.0f);
+        break;
+    }
+    }
+    return __all(ok);
+}
+
 // Runtime program: the program counter, op and stack pointers are
 // wave-uniform (every lane runs the same program), so the stacks stay in
-// registers indexed by SGPR values.
+// registers indexed by SGPR values.  A guarded operand is skipped when its
+// guard holds for the whole wave.
 struct SdfProgram {
     const rrte_sdf_node* __restrict__ nodes;
     uint32_t count;
@@ -274,25 +310,49 @@ struct SdfProgram {
         float vs[RRTE_SDF_MAX_STACK];
         f3 ps[RRTE_SDF_MAX_POINT_STACK];
         uint32_t sp = 0, pp = 0;
-        for (uint32_t i = 0; i < count; ++i) sdf_node_step(nodes[i], vs, ps, sp, pp, p);
+        for (uint32_t i = 0; i < count; ++i) {
+            const uint32_t link = nodes[i].i[2];
+            float r;
+            if (link != 0u && sdf_guard(nodes[link - 1u], vs[sp - 1], p, r)) {
+                vs[sp - 1] = r;
+                i = link - 1u;  // continue after the op
+                continue;
+            }
+            sdf_node_step(nodes[i], vs, ps, sp, pp, p);
+        }
         return vs[0];
     }
 };
 
 // Static program (scene-specialised kernel): nodes [FIRST, FIRST+COUNT) of a
 // constexpr scene, unrolled at compile time; ops fold, stack slots become
-// fixed registers.
+// fixed registers.  A guarded operand [I, J) becomes a uniform branch around
+// its straight-line code.
+template <class S, uint32_t FIRST, uint32_t I, uint32_t END, bool CHECK>
+__device__ __forceinline__ void sdf_static_range(float* vs, f3* ps, uint32_t& sp, uint32_t& pp, f3& p) {
+    if constexpr (I < END) {
+        constexpr rrte_sdf_node n = S::nodes[FIRST + I];
+        constexpr uint32_t link = n.i[2];
+        if constexpr (CHECK && link != 0u) {
+            constexpr rrte_sdf_node g = S::nodes[FIRST + link - 1u];
+            float r;
+            if (sdf_guard(g, vs[sp - 1], p, r)) vs[sp - 1] = r;
+            else sdf_static_range<S, FIRST, I, link, false>(vs, ps, sp, pp, p);
+            sdf_static_range<S, FIRST, link, END, true>(vs, ps, sp, pp, p);
+        } else {
+            sdf_node_step(n, vs, ps, sp, pp, p);
+            sdf_static_range<S, FIRST, I + 1u, END, true>(vs, ps, sp, pp, p);
+        }
+    }
+}
+
 template <class S, uint32_t FIRST, uint32_t COUNT>
 struct SdfStaticProgram {
     __device__ __forceinline__ float operator()(f3 p) const {
         float vs[RRTE_SDF_MAX_STACK];
         f3 ps[RRTE_SDF_MAX_POINT_STACK];
         uint32_t sp = 0, pp = 0;
-        auto step = [&](auto jj) {
-            constexpr rrte_sdf_node n = S::nodes[FIRST + decltype(jj)::value];
-            sdf_node_step(n, vs, ps, sp, pp, p);
-        };
-        static_for<0, COUNT>(step);
+        sdf_static_range<S, FIRST, 0u, COUNT, true>(vs, ps, sp, pp, p);
         return vs[0];
     }
 };

@@ -23,6 +23,7 @@
 
 #include "bvh.hpp"
 #include "jit.hpp"
+#include "sdf_guard.hpp"
 #include "ray_kernels.hpp"
 
 using namespace rrte;
@@ -79,6 +80,7 @@ struct rrte_ctx {
     uint32_t env_debug = 0;       // RRTE_DEBUG ablation bits
     int env_cull = -1;            // RRTE_CULL: -1 unset, 0 off, 1 on
     bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
+    uint32_t env_guard_leaves = 2;  // RRTE_CSG_GUARDS: 0 = off, N = smallest guarded operand (leaves)
     int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, valid; JitKernel* k; } jit_last{};
@@ -426,7 +428,9 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     if ((r = put(c->d_prims, prims.data(), prims.size() * sizeof(DPrim))) != RRTE_OK) return r;
     if ((r = put(c->d_mats, mats.data(), mats.size() * sizeof(DMaterial))) != RRTE_OK) return r;
     if ((r = put(c->d_lights, lights.data(), lights.size() * sizeof(DLight))) != RRTE_OK) return r;
-    if ((r = put(c->d_nodes, s->sdf_nodes, bn)) != RRTE_OK) return r;
+    // SDF programs with their exact CSG early-outs (sdf_guard.hpp); the key above stays the caller's IR
+    std::vector<rrte_sdf_node> nodes = decorate_scene_sdf(s, c->env_guard_leaves);
+    if ((r = put(c->d_nodes, nodes.data(), bn)) != RRTE_OK) return r;
     if ((r = put(c->d_bounds, bounds.data(), bounds.size() * sizeof(float4))) != RRTE_OK) return r;
     if ((r = put(c->d_mesh_nodes, md.nodes.data(), md.nodes.size() * sizeof(float4))) != RRTE_OK) return r;
     if ((r = put(c->d_mesh_tris, md.tris.data(), md.tris.size() * sizeof(float4))) != RRTE_OK) return r;
@@ -443,7 +447,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     c->h_prims = prims;
     c->h_mats = mats;
     c->h_lights = lights;
-    c->h_nodes.assign(s->sdf_nodes, s->sdf_nodes + s->num_sdf_nodes);
+    c->h_nodes = std::move(nodes);
     c->n_prims = s->num_prims;
     c->n_mats = s->num_materials;
     c->n_lights = s->num_lights;
@@ -509,6 +513,12 @@ uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank
 // so scenes of <= 64 objects; it pays where an occlusion test is expensive (sphere-traced SDF
 // objects) and costs a few percent on all-analytic scenes (measured).  RRTE_CULL=0/1
 // forces it off/on (A/B runs, tests).
+// RRTE_CSG_GUARDS: unset = 2 (guard operands of >= 2 leaves), 0 = off, N = smallest guarded operand
+uint32_t env_guard_setting() {
+    const char* g = getenv("RRTE_CSG_GUARDS");
+    return g ? (uint32_t)strtoul(g, nullptr, 0) : 2u;
+}
+
 int env_cull_setting() {
     const char* ce = getenv("RRTE_CULL");
     return ce ? (ce[0] != '0' ? 1 : 0) : -1;
@@ -721,6 +731,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* d = getenv("RRTE_DEBUG")) c->env_debug = (uint32_t)strtoul(d, nullptr, 0);
     c->env_cull = env_cull_setting();
     if (const char* g = getenv("RRTE_FORCE_GATHER")) c->env_force_gather = g[0] == '1';
+    c->env_guard_leaves = env_guard_setting();
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
         if (sscanf(e, "%d:%d", &n, &r) == 2 && n > 1 && r >= 0 && r < n) {
@@ -841,6 +852,16 @@ rrte_status rrte_hip_stats(rrte_ctx* c, rrte_stats* out) {
     return RRTE_OK;
 }
 
+rrte_status rrte_hip_sdf_guards(const rrte_sdf_node* in, uint32_t count, uint32_t min_leaves, rrte_sdf_node* out,
+                                uint32_t* guards) {
+    if ((count && (!in || !out)) || !guards) return RRTE_INVALID_ARG;
+    if (count && !sdf_program_ok(in, count)) return RRTE_UNSUPPORTED_PRIM;
+    if (count) memmove(out, in, sizeof(rrte_sdf_node) * count);
+    for (uint32_t i = 0; i < count; ++i) out[i].i[kGuardSlot] = 0u;
+    *guards = min_leaves && count ? decorate_sdf_guards(out, count, min_leaves) : 0u;
+    return RRTE_OK;
+}
+
 rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size_t log_len) {
     if (!s || (s->num_prims && !s->prims) || (s->num_sdf_nodes && !s->sdf_nodes)) return RRTE_INVALID_ARG;
     std::vector<DPrim> prims;
@@ -854,8 +875,9 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
     // spp > 1 or max_depth > 1) instead of the straight-line one
     const char* mv = getenv("RRTE_JIT_CHECK_MULTI");
     const bool single = !(mv && mv[0] == '1');
+    const std::vector<rrte_sdf_node> nodes = decorate_scene_sdf(s, env_guard_setting());
     std::string src = jit_source(prims.data(), (uint32_t)prims.size(), mats.data(), (uint32_t)mats.size(),
-                                 lights.data(), (uint32_t)lights.size(), s->sdf_nodes, s->num_sdf_nodes, mode,
+                                 lights.data(), (uint32_t)lights.size(), nodes.data(), s->num_sdf_nodes, mode,
                                  cull_policy(s, (uint32_t)mode, env_cull_setting()), single);
     std::string msg;
     bool ok = jit_compile_only(src, msg);

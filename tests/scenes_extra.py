@@ -101,3 +101,46 @@ def cull_stress_scene(w, h, mode, n_spheres=40, seed=7):
     cfg = RaytracerConfig(max_depth=1, samples_per_pixel=1, width=w, height=h, jitter="center", mode=mode,
                           background_color=Color(0.1, 0.1, 0.15, 1))
     return objs, lights, cam, cfg
+
+
+def random_csg_scene(w, h, mode, seed=11, n_objects=4, depth=4):
+    """SDF objects built from random CSG trees over every leaf kind and every op (smooth k random),
+    some subtrees under deformers: exercises the CSG early-outs (sdf_guard.hip) at every nesting."""
+    import numpy as np
+    from rrte_amd import renderer as R
+
+    rng = np.random.default_rng(seed)
+    ops = ["union", "smooth_union", "difference", "smooth_difference", "intersection", "smooth_intersection"]
+
+    def leaf(c):
+        k = int(rng.integers(10))
+        s = float(rng.uniform(0.3, 0.9))
+        c = tuple(float(v) for v in c)
+        return [R.SDFSphere(c, s), R.SDFBox(c, (s * 1.5, s, s * 1.2)), R.SDFCylinder(c, s * 0.6, s * 1.6),
+                R.SDFPrism(c, (s, s * 1.5, s)), R.SDFTorus(c, s, s * 0.3), R.SDFTube(c, s, s * 0.6, s * 1.4),
+                R.SDFRing(c, s, s * 0.25), R.SDFCone(c, s * 0.7, s * 1.5), R.SDFCapsule(c, s * 0.4, s),
+                R.SDFEllipsoid(c, (s, s * 0.3, s * 0.8))][k]
+
+    def tree(c, d):
+        if d == 0 or rng.uniform() < 0.15:
+            return leaf(c)
+        spread = 0.35 * d
+        a = tree(np.asarray(c) + rng.uniform(-spread, spread, 3), d - 1)
+        b = tree(np.asarray(c) + rng.uniform(-spread, spread, 3), d - 1)
+        t = R.CSGComposite(a, b, ops[int(rng.integers(6))] if d < depth else "union", float(rng.uniform(0.05, 0.5)))
+        if d == 2 and rng.uniform() < 0.3:
+            t = R.DeformedSDF(t, R.TwistDeformer((0, 1, 0), float(rng.uniform(0.2, 0.8)), tuple(c)))
+        return t
+
+    m = [LambertianMaterial(Color.rgb(0.7, 0.5, 0.3)), LambertianMaterial(Color.rgb(0.3, 0.6, 0.8))]
+    objs = [Sphere((0.0, -1000.0, 0.0), 1000.0, LambertianMaterial(Color.rgb(0.2, 0.2, 0.2)))]
+    for i in range(n_objects):
+        c = (-4.5 + 3.0 * i, 1.8, float(rng.uniform(-1, 1)))
+        objs.append(SDFObject(tree(c, depth), m[i % 2], max_steps=160))
+    lights = [PointLight((0, 8, 6), Color.rgb(1, 1, 1), 25.0), PointLight((-6, 5, -3), Color.rgb(1, 0.8, 0.6), 15.0)]
+    cam = Camera.new_perspective(to_radians(45.0), f32(w) / f32(h), 0.1, 100.0)
+    cam.transform.position = vec3(0, 4, 12)
+    cam.look_at((0, 1.5, 0))
+    cfg = RaytracerConfig(max_depth=1, samples_per_pixel=1, width=w, height=h, jitter="center", mode=mode,
+                          background_color=Color(0.05, 0.05, 0.08, 1))
+    return objs, lights, cam, cfg
