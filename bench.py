@@ -149,6 +149,18 @@ def pmc_traffic(workload_key):
     return best
 
 
+def measured_valu_peak():
+    """Wave64 VALU issue rates measured on MI355X by tools/valu_peak.hip (profiles/r01_valu_peak.json):
+    FMA-class (v_fma/v_add/v_mul_f32) and compare/select-class (v_cmp, v_cndmask_e64, v_max_f32)."""
+    f = ROOT / "profiles" / "r01_valu_peak.json"
+    if not f.exists():
+        return None
+    ops = {o["op"]: o["wave_instr_per_s"] for o in json.loads(f.read_text())["ops"]}
+    fma = statistics.mean(ops[k] for k in ("v_fma_f32", "v_add_f32", "v_mul_f32"))
+    sel = statistics.mean(ops[k] for k in ("v_cmp_lt_f32(vcc)", "v_cndmask_b32_e64 s[20:21]", "v_max_f32"))
+    return {"fma_add_mul": fma, "cmp_select_max": sel, "source": "profiles/r01_valu_peak.json"}
+
+
 def stock_config(args):
     """The reference's own default workload on the same scene (SURVEY §8d secondary number):
     REFCOMPAT, spp 4, max_depth 50, random jitter and scatter (counter-based RNG)."""
@@ -317,7 +329,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if world > 1 else "weak",
+            "scaling": "strong",  # one 1080p frame per step whatever N: total work fixed
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
@@ -354,7 +366,14 @@ def main():
         line["frame_latency_ms"] = round(latency_ms, 4)
         line["d2h_ms"] = round(d2h_ms, 4)  # frame to pinned host memory, excluded from `value`
         if pmc and pmc.get("valu") is not None:
-            line["valu"] = pmc["valu"]
+            line["valu"] = dict(pmc["valu"])
+            mp = measured_valu_peak()
+            if mp:
+                # the PMC issue rate against the MEASURED wave64 issue rates of this chip (tools/valu_peak.hip)
+                r = line["valu"]["wave_instr_per_s"]
+                line["valu"]["measured_peak"] = mp
+                line["valu"]["frac_of_measured_fma_class_peak"] = r / mp["fma_add_mul"]
+                line["valu"]["frac_of_measured_cmp_select_peak"] = r / mp["cmp_select_max"]
         if stock is not None:
             line["stock_config"] = stock
         if world == 1 and not args.no_cpu:
