@@ -58,6 +58,13 @@ static inline v3 setcomp(v3 a, int i, float s) {
 static inline float mn(float a, float b) { return (b < a) ? b : a; }
 static inline float mx(float a, float b) { return (b > a) ? b : a; }
 static inline float clampf_(float x, float lo, float hi) { return mn(mx(x, lo), hi); }
+/* SDF min/max (build-defined): IEEE-754 minNum/maxNum -- a NaN operand yields the
+ * other operand -- which the device evaluates with single v_min_f32/v_max_f32/v_max3_f32/v_med3_f32
+ * instructions.  The sign of a zero result when both operands are zeros is unspecified (the device
+ * compiler may reassociate); no SDF output depends on it (a distance of +-0 marches and shades alike). */
+static inline float smn(float a, float b) { return fminf(a, b); }
+static inline float smx(float a, float b) { return fmaxf(a, b); }
+static inline float sclamp(float x, float lo, float hi) { return smn(smx(x, lo), hi); }
 
 /* ------------------------------------------------------- rrte_math types */
 typedef struct ray { v3 o, d; } ray;
@@ -275,17 +282,17 @@ static float sdf_leaf(const rrte_sdf_node* n, v3 p) {
         return len3f(q.x, q.y, q.z) - f[3];
     case RRTE_SDF_BOX: {
         float dx = fabsf(q.x) - f[4] * 0.5f, dy = fabsf(q.y) - f[5] * 0.5f, dz = fabsf(q.z) - f[6] * 0.5f;
-        float outside = len3f(mx(dx, 0.0f), mx(dy, 0.0f), mx(dz, 0.0f));
-        float inside = mn(mx(dx, mx(dy, dz)), 0.0f);
+        float outside = len3f(smx(dx, 0.0f), smx(dy, 0.0f), smx(dz, 0.0f));
+        float inside = smn(smx(dx, smx(dy, dz)), 0.0f);
         return outside + inside;
     }
     case RRTE_SDF_CYLINDER: {
         float dx = len2f(q.x, q.z) - f[3], dy = fabsf(q.y) - f[4] * 0.5f;
-        return mn(mx(dx, dy), 0.0f) + len2f(mx(dx, 0.0f), mx(dy, 0.0f));
+        return smn(smx(dx, dy), 0.0f) + len2f(smx(dx, 0.0f), smx(dy, 0.0f));
     }
     case RRTE_SDF_PRISM: {
-        float a = mx(fabsf(q.x) * 0.866025f + q.y * 0.5f, -q.y) - f[5] * 0.25f;
-        return mx(fabsf(q.z) - f[6] * 0.5f, a);
+        float a = smx(fabsf(q.x) * 0.866025f + q.y * 0.5f, -q.y) - f[5] * 0.25f;
+        return smx(fabsf(q.z) - f[6] * 0.5f, a);
     }
     case RRTE_SDF_TORUS: {
         float qx = len2f(q.x, q.z) - f[3];
@@ -295,7 +302,7 @@ static float sdf_leaf(const rrte_sdf_node* n, v3 p) {
         float rad = len2f(q.x, q.z);
         float mid = (f[3] + f[4]) * 0.5f, half = (f[3] - f[4]) * 0.5f;
         float dx = fabsf(rad - mid) - half, dy = fabsf(q.y) - f[5] * 0.5f;
-        return mn(mx(dx, dy), 0.0f) + len2f(mx(dx, 0.0f), mx(dy, 0.0f));
+        return smn(smx(dx, dy), 0.0f) + len2f(smx(dx, 0.0f), smx(dy, 0.0f));
     }
     case RRTE_SDF_RING: {
         float qx = len2f(q.x, q.y) - f[3];
@@ -306,28 +313,28 @@ static float sdf_leaf(const rrte_sdf_node* n, v3 p) {
         float r1 = f[3], hh = f[4] * 0.5f;
         float qx = len2f(q.x, q.z), qy = q.y;
         float k2x = -r1, k2y = hh * 2.0f;
-        float cax = qx - mn(qx, (qy < 0.0f) ? r1 : 0.0f);
+        float cax = qx - smn(qx, (qy < 0.0f) ? r1 : 0.0f);
         float cay = fabsf(qy) - hh;
         float k1mqx = 0.0f - qx, k1mqy = hh - qy;
         float tnum = k1mqx * k2x + k1mqy * k2y;
         float tden = k2x * k2x + k2y * k2y;
-        float t = clampf_(tnum / tden, 0.0f, 1.0f);
+        float t = sclamp(tnum / tden, 0.0f, 1.0f);
         float cbx = (qx - 0.0f) + k2x * t;
         float cby = (qy - hh) + k2y * t;
         float s = (cbx < 0.0f && cay < 0.0f) ? -1.0f : 1.0f;
         float da = cax * cax + cay * cay, db = cbx * cbx + cby * cby;
-        return s * sqrtf(mn(da, db));
+        return s * sqrtf(smn(da, db));
     }
     case RRTE_SDF_CAPSULE: {
         float hh = f[4] * 0.5f;
-        float y = q.y - clampf_(q.y, -hh, hh);
+        float y = q.y - sclamp(q.y, -hh, hh);
         return len3f(q.x, y, q.z) - f[3];
     }
     case RRTE_SDF_ELLIPSOID: {
         float rx = f[4], ry = f[5], rz = f[6];
         float k0 = len3f(q.x / rx, q.y / ry, q.z / rz);
         float k1 = len3f(q.x / (rx * rx), q.y / (ry * ry), q.z / (rz * rz));
-        if (!(k1 > 0.0f)) return -mn(rx, mn(ry, rz));
+        if (!(k1 > 0.0f)) return -smn(rx, smn(ry, rz));
         return k0 * (k0 - 1.0f) / k1;
     }
     default:
@@ -337,7 +344,7 @@ static float sdf_leaf(const rrte_sdf_node* n, v3 p) {
 
 /* smooth_min (README.md:485-488): h = clamp(0.5 + 0.5 (b-a)/k); a h + b (1-h) - k h (1-h). */
 static inline float smin(float a, float b, float k) {
-    float h = clampf_(0.5f + (0.5f * (b - a)) / k, 0.0f, 1.0f);
+    float h = sclamp(0.5f + (0.5f * (b - a)) / k, 0.0f, 1.0f);
     float om = 1.0f - h;
     return (a * h + b * om) - (k * h) * om;
 }
@@ -362,7 +369,7 @@ static v3 sdf_deform(const rrte_sdf_node* n, v3 p) {
     case RRTE_SDF_TAPER: {
         int ax = (int)n->i[0];
         int u = (ax + 1) % 3, w = (ax + 2) % 3;
-        float t = clampf_((comp(q, ax) + f[5] * 0.5f) / f[5], 0.0f, 1.0f);
+        float t = sclamp((comp(q, ax) + f[5] * 0.5f) / f[5], 0.0f, 1.0f);
         float s = f[3] + (f[4] - f[3]) * t;
         q = setcomp(q, u, comp(q, u) / s);
         q = setcomp(q, w, comp(q, w) / s);
@@ -412,9 +419,9 @@ static float sdf_eval(const rrte_sdf_node* nodes, uint32_t count, v3 p) {
         } else if (op < 64) {
             float b = vs[--sp], a = vs[--sp], r;
             switch (op) {
-            case RRTE_SDF_UNION: r = mn(a, b); break;
-            case RRTE_SDF_DIFFERENCE: r = mx(a, -b); break;
-            case RRTE_SDF_INTERSECTION: r = mx(a, b); break;
+            case RRTE_SDF_UNION: r = smn(a, b); break;
+            case RRTE_SDF_DIFFERENCE: r = smx(a, -b); break;
+            case RRTE_SDF_INTERSECTION: r = smx(a, b); break;
             case RRTE_SDF_SMOOTH_UNION: r = smin(a, b, n->f[0]); break;
             case RRTE_SDF_SMOOTH_DIFFERENCE: r = -smin(-a, b, n->f[0]); break;
             default: r = -smin(-a, -b, n->f[0]); break; /* SMOOTH_INTERSECTION */

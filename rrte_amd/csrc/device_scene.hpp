@@ -155,6 +155,12 @@ __device__ __forceinline__ f3 setcomp(f3 a, uint32_t i, float s) {
 __device__ __forceinline__ float mn(float a, float b) { return (b < a) ? b : a; }
 __device__ __forceinline__ float mx(float a, float b) { return (b > a) ? b : a; }
 __device__ __forceinline__ float clampf_(float x, float lo, float hi) { return mn(mx(x, lo), hi); }
+// SDF min/max (build-defined): IEEE-754 minNum/maxNum (a NaN operand yields the other),
+// one v_min_f32 / v_max_f32 / v_max3_f32 / v_med3_f32 each instead of a compare + select; the oracle's
+// smn/smx are fminf/fmaxf.  Zero-sign of a +-0 tie unspecified (no SDF output depends on it).
+__device__ __forceinline__ float smn(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ float smx(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ float sclamp(float x, float lo, float hi) { return smn(smx(x, lo), hi); }
 
 struct Ray { f3 o, d; };
 // Ray::new normalises (ray.rs:13-18); Ray::at (ray.rs:21-23)

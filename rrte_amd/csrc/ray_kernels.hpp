@@ -108,17 +108,17 @@ __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__
         return len3f(q.x, q.y, q.z) - f[3];
     case RRTE_SDF_BOX: {
         float dx = fabsf(q.x) - f[4] * 0.5f, dy = fabsf(q.y) - f[5] * 0.5f, dz = fabsf(q.z) - f[6] * 0.5f;
-        float outside = len3f(mx(dx, 0.0f), mx(dy, 0.0f), mx(dz, 0.0f));
-        float inside = mn(mx(dx, mx(dy, dz)), 0.0f);
+        float outside = len3f(smx(dx, 0.0f), smx(dy, 0.0f), smx(dz, 0.0f));
+        float inside = smn(smx(dx, smx(dy, dz)), 0.0f);
         return outside + inside;
     }
     case RRTE_SDF_CYLINDER: {
         float dx = len2f(q.x, q.z) - f[3], dy = fabsf(q.y) - f[4] * 0.5f;
-        return mn(mx(dx, dy), 0.0f) + len2f(mx(dx, 0.0f), mx(dy, 0.0f));
+        return smn(smx(dx, dy), 0.0f) + len2f(smx(dx, 0.0f), smx(dy, 0.0f));
     }
     case RRTE_SDF_PRISM: {
-        float a = mx(fabsf(q.x) * 0.866025f + q.y * 0.5f, -q.y) - f[5] * 0.25f;
-        return mx(fabsf(q.z) - f[6] * 0.5f, a);
+        float a = smx(fabsf(q.x) * 0.866025f + q.y * 0.5f, -q.y) - f[5] * 0.25f;
+        return smx(fabsf(q.z) - f[6] * 0.5f, a);
     }
     case RRTE_SDF_TORUS: {
         float qx = len2f(q.x, q.z) - f[3];
@@ -128,7 +128,7 @@ __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__
         float rad = len2f(q.x, q.z);
         float mid = (f[3] + f[4]) * 0.5f, half = (f[3] - f[4]) * 0.5f;
         float dx = fabsf(rad - mid) - half, dy = fabsf(q.y) - f[5] * 0.5f;
-        return mn(mx(dx, dy), 0.0f) + len2f(mx(dx, 0.0f), mx(dy, 0.0f));
+        return smn(smx(dx, dy), 0.0f) + len2f(smx(dx, 0.0f), smx(dy, 0.0f));
     }
     case RRTE_SDF_RING: {
         float qx = len2f(q.x, q.y) - f[3];
@@ -138,28 +138,28 @@ __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__
         float r1 = f[3], hh = f[4] * 0.5f;
         float qx = len2f(q.x, q.z), qy = q.y;
         float k2x = -r1, k2y = hh * 2.0f;
-        float cax = qx - mn(qx, (qy < 0.0f) ? r1 : 0.0f);
+        float cax = qx - smn(qx, (qy < 0.0f) ? r1 : 0.0f);
         float cay = fabsf(qy) - hh;
         float k1mqx = 0.0f - qx, k1mqy = hh - qy;
         float tnum = k1mqx * k2x + k1mqy * k2y;
         float tden = k2x * k2x + k2y * k2y;
-        float t = clampf_(div_rn(tnum, tden), 0.0f, 1.0f);
+        float t = sclamp(div_rn(tnum, tden), 0.0f, 1.0f);
         float cbx = (qx - 0.0f) + k2x * t;
         float cby = (qy - hh) + k2y * t;
         float s = (cbx < 0.0f && cay < 0.0f) ? -1.0f : 1.0f;
         float da = cax * cax + cay * cay, db = cbx * cbx + cby * cby;
-        return s * sqrt_rn(mn(da, db));
+        return s * sqrt_rn(smn(da, db));
     }
     case RRTE_SDF_CAPSULE: {
         float hh = f[4] * 0.5f;
-        float y = q.y - clampf_(q.y, -hh, hh);
+        float y = q.y - sclamp(q.y, -hh, hh);
         return len3f(q.x, y, q.z) - f[3];
     }
     case RRTE_SDF_ELLIPSOID: {
         float rx = f[4], ry = f[5], rz = f[6];
         float k0 = len3f(div_rn(q.x, rx), div_rn(q.y, ry), div_rn(q.z, rz));
         float k1 = len3f(div_rn(q.x, rx * rx), div_rn(q.y, ry * ry), div_rn(q.z, rz * rz));
-        if (!(k1 > 0.0f)) return -mn(rx, mn(ry, rz));
+        if (!(k1 > 0.0f)) return -smn(rx, smn(ry, rz));
         return k0 * (k0 - 1.0f) / k1;
     }
     default:
@@ -169,7 +169,7 @@ __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__
 
 // smooth_min (README.md:485-488)
 __device__ __forceinline__ float smin(float a, float b, float k) {
-    float h = clampf_(0.5f + div_rn(0.5f * (b - a), k), 0.0f, 1.0f);
+    float h = sclamp(0.5f + div_rn(0.5f * (b - a), k), 0.0f, 1.0f);
     float om = 1.0f - h;
     return (a * h + b * om) - (k * h) * om;
 }
@@ -194,7 +194,7 @@ __device__ __forceinline__ f3 sdf_deform(uint32_t op, const uint32_t* __restrict
     case RRTE_SDF_TAPER: {
         uint32_t ax = iarg[0];
         uint32_t u = (ax + 1) % 3, w = (ax + 2) % 3;
-        float t = clampf_(div_rn(comp(q, ax) + f[5] * 0.5f, f[5]), 0.0f, 1.0f);
+        float t = sclamp(div_rn(comp(q, ax) + f[5] * 0.5f, f[5]), 0.0f, 1.0f);
         float s = f[3] + (f[4] - f[3]) * t;
         q = setcomp(q, u, comp(q, u) / s);
         q = setcomp(q, w, comp(q, w) / s);
@@ -244,9 +244,9 @@ __device__ __forceinline__ void sdf_node_step(const rrte_sdf_node& n, float* vs,
         float b = vs[sp - 1], a = vs[sp - 2], r;
         float k = n.f[0];
         switch (op) {
-        case RRTE_SDF_UNION: r = mn(a, b); break;
-        case RRTE_SDF_DIFFERENCE: r = mx(a, -b); break;
-        case RRTE_SDF_INTERSECTION: r = mx(a, b); break;
+        case RRTE_SDF_UNION: r = smn(a, b); break;
+        case RRTE_SDF_DIFFERENCE: r = smx(a, -b); break;
+        case RRTE_SDF_INTERSECTION: r = smx(a, b); break;
         case RRTE_SDF_SMOOTH_UNION: r = smin(a, b, k); break;
         case RRTE_SDF_SMOOTH_DIFFERENCE: r = -smin(-a, b, k); break;
         default: r = -smin(-a, -b, k); break;
@@ -286,12 +286,12 @@ __device__ __forceinline__ bool sdf_guard(const rrte_sdf_node& g, float a, f3 p,
         r = a;
         break;
     case RRTE_SDF_SMOOTH_UNION:
-        ok = ok && clampf_(0.5f + div_rn(0.5f * (L - a), g.f[0]), 0.0f, 1.0f) == 1.0f;
+        ok = ok && sclamp(0.5f + div_rn(0.5f * (L - a), g.f[0]), 0.0f, 1.0f) == 1.0f;
         r = a + 0.0f;
         break;
     default: {  // RRTE_SDF_SMOOTH_DIFFERENCE: -smin(-a, b, k)
         const float na = -a;
-        ok = ok && clampf_(0.5f + div_rn(0.5f * (L - na), g.f[0]), 0.0f, 1.0f) == 1.0f;
+        ok = ok && sclamp(0.5f + div_rn(0.5f * (L - na), g.f[0]), 0.0f, 1.0f) == 1.0f;
         r = -(na + 0.0f);
         break;
     }

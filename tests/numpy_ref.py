@@ -369,8 +369,8 @@ def sdf_leaf(op, f, p):
     q = [p[k] - f[k] for k in range(3)]
     l2 = lambda a, b: np.sqrt(a * a + b * b)  # noqa: E731
     l3 = lambda a, b, c: np.sqrt((a * a + b * b) + c * c)  # noqa: E731
-    mx = lambda a, b: np.where(b > a, b, a)  # noqa: E731
-    mn = lambda a, b: np.where(b < a, b, a)  # noqa: E731
+    # SDF min/max are IEEE minNum/maxNum (a NaN operand yields the other): np.fmax / np.fmin
+    mx, mn = np.fmax, np.fmin
     Z = F(0)
     if op == abi.SDF_SPHERE:
         return l3(*q) - f[3]
@@ -399,6 +399,6 @@ def sdf_leaf(op, f, p):
 def smin(a, b, k):
     k = F(k)
     h = (F(0.5) + (F(0.5) * (b - a)) / k)
-    h = np.where(F(1) < np.where(F(0) > h, F(0), h), F(1), np.where(F(0) > h, F(0), h))
+    h = np.fmin(np.fmax(h, F(0)), F(1))
     om = F(1) - h
     return (a * h + b * om) - (k * h) * om
