@@ -78,6 +78,12 @@ struct KParams {
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
 };
 
+// Internal KParams::flags bit (never in the public rrte_render_params::flags): the launch writes
+// a gather slab of packed RGB24 pixels (3 B, alpha dropped) instead of RGBA8.  The host sets it
+// only when it has proved every pixel's alpha byte is 255 (rrte_hip.hip, slab_rgb24), and the
+// root's de-interleave puts the 255 back.
+constexpr uint32_t kFlagSlabRgb24 = 1u << 31;
+
 // ---------------------------------------------------------------- f32 vec3
 struct f3 { float x, y, z; };
 

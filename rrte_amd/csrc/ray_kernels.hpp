@@ -1417,8 +1417,17 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
         float gr = rclamp(powf(acc.r, ig)), gg = rclamp(powf(acc.g, ig)), gb = rclamp(powf(acc.b, ig));
         float ga = rclamp(acc.a);
         const size_t o = (size_t)lr * kp.width + x;  // packed local rows
-        if (out_rgba8)
-            out_rgba8[o] = to_u8(gr) | (to_u8(gg) << 8) | (to_u8(gb) << 16) | (to_u8(ga) << 24);
+        if (out_rgba8) {
+            const uint32_t px = to_u8(gr) | (to_u8(gg) << 8) | (to_u8(gb) << 16) | (to_u8(ga) << 24);
+            if (kp.flags & kFlagSlabRgb24) {  // gather slab, alpha proven 255: 3 bytes per pixel
+                uint8_t* b = reinterpret_cast<uint8_t*>(out_rgba8) + 3u * o;
+                b[0] = (uint8_t)px;
+                b[1] = (uint8_t)(px >> 8);
+                b[2] = (uint8_t)(px >> 16);
+            } else {
+                out_rgba8[o] = px;
+            }
+        }
         if (out_f32) {
             if (kp.flags & RRTE_FLAG_F32_LINEAR)
                 out_f32[o] = make_float4(acc.r, acc.g, acc.b, acc.a);
@@ -1448,20 +1457,28 @@ __global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, Cull
     ray_kernel_body<MODE, SceneView, false, CULL>(kp, sc, cl, out_rgba8, out_f32, counters);
 }
 
-// Root-side de-interleave after the RCCL gather: the gathered buffer holds
-// each rank's packed rows (rank-major, `rows_cap` rows per rank).
-__global__ __launch_bounds__(256) void deinterleave_kernel(const uint32_t* __restrict__ gathered,
+// Root-side de-interleave after the RCCL gather: the gathered buffer holds each rank's packed
+// rows (rank-major, one `slice` of bytes per rank, `rows_cap` rows of RGBA8 or RGB24 each).
+// RGB24 slabs are expanded with alpha 255 (the host proved every alpha byte is 255).
+template <bool RGB24>
+__global__ __launch_bounds__(256) void deinterleave_kernel(const uint8_t* __restrict__ gathered,
                                                            uint32_t* __restrict__ full, uint32_t width,
-                                                           uint32_t height, uint32_t band_rows,
-                                                           uint32_t nranks, uint32_t rows_cap) {
+                                                           uint32_t band_rows, uint32_t nranks, size_t slice) {
     const uint32_t y = blockIdx.y;
     const uint32_t band = y / band_rows, w = y - band * band_rows;
     const uint32_t rank = band % nranks, local_band = band / nranks;
     const uint32_t lr = local_band * band_rows + w;
-    const uint32_t* src = gathered + ((size_t)rank * rows_cap + lr) * width;
+    constexpr uint32_t bpp = RGB24 ? 3u : 4u;
+    const uint8_t* src = gathered + (size_t)rank * slice + (size_t)lr * width * bpp;
     uint32_t* dst = full + (size_t)y * width;
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < width; x += gridDim.x * blockDim.x) dst[x] = src[x];
-    (void)height;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < width; x += gridDim.x * blockDim.x) {
+        if constexpr (RGB24) {
+            const uint8_t* q = src + 3u * x;
+            dst[x] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | 0xFF000000u;
+        } else {
+            dst[x] = reinterpret_cast<const uint32_t*>(src)[x];
+        }
+    }
 }
 
 }  // namespace rrte

@@ -80,6 +80,7 @@ struct rrte_ctx {
     uint32_t env_debug = 0;       // RRTE_DEBUG ablation bits
     int env_cull = -1;            // RRTE_CULL: -1 unset, 0 off, 1 on
     bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
+    bool env_gather_rgba = false;   // RRTE_GATHER_RGB24=0: gather slabs always RGBA8
     uint32_t env_guard_leaves = 2;  // RRTE_CSG_GUARDS: 0 = off, N = smallest guarded operand (leaves)
     int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
@@ -601,8 +602,9 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
 }
 
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
-                   uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
+                   uint32_t* d_rgba, float4* d_f32, hipStream_t st, uint32_t internal_flags = 0u) {
     KParams k = make_params(c, s, p, rows);
+    k.flags |= internal_flags;
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, s->num_prims, s->num_lights, s->num_materials,
                  c->mesh_view};
     const bool cull = cull_policy(s, p->mode, c->env_cull);
@@ -731,6 +733,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* d = getenv("RRTE_DEBUG")) c->env_debug = (uint32_t)strtoul(d, nullptr, 0);
     c->env_cull = env_cull_setting();
     if (const char* g = getenv("RRTE_FORCE_GATHER")) c->env_force_gather = g[0] == '1';
+    if (const char* g = getenv("RRTE_GATHER_RGB24")) c->env_gather_rgba = g[0] == '0';
     c->env_guard_leaves = env_guard_setting();
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
@@ -958,6 +961,23 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
     return RRTE_OK;
 }
 
+// Gather slabs carry RGB24 (3 B/pixel, 25 % fewer bytes over xGMI) when every pixel's alpha byte
+// is provably 255.  LAMBERT_SHADOW never lets a light touch alpha (ray_kernels.hpp, shade_lambert):
+// a sample's alpha is the background's (miss), 1 (no material, max_depth 0) or 1 + (a*0.1)*0.1 for
+// the material's albedo alpha a, and the pixel's is rclamp((1 + sum of sample alphas) * inv_spp)
+// (the sum starts from BLACK, alpha 1).  With every sample alpha >= 0 (spp 1) or >= 1 (spp n > 1:
+// the sum is then >= n + 1 and (n + 1) * RN(1/n) >= 1), the clamp gives 1.0 and to_u8 255.  The
+// test is on signs only (no host arithmetic to mirror); NaN fails it.  Every rank decides from the
+// same scene and parameters, so all agree on the slab format.  RRTE_GATHER_RGB24=0 forces RGBA8.
+bool slab_rgb24(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p) {
+    if (c->env_gather_rgba || c->env_debug || p->mode != RRTE_MODE_LAMBERT_SHADOW) return false;
+    const float thr = p->samples_per_pixel == 1 ? 0.0f : 1.0f;
+    if (!(p->background[3] >= thr)) return false;
+    for (uint32_t i = 0; i < s->num_materials; ++i)
+        if (!(s->materials[i].albedo[3] >= 0.0f)) return false;
+    return true;
+}
+
 rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
                                          void* d_full, void* stream) {
     if (!c) return RRTE_INVALID_ARG;
@@ -973,7 +993,10 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
     pp.band_rows = band;
     const uint32_t rows = rows_for_rank(p->height, band, c->nranks, c->rank);
     const uint32_t cap = rows_for_rank(p->height, band, c->nranks, 0);  // rank 0 owns the most rows
-    const size_t slice = (size_t)cap * p->width;
+    const bool rgb24 = slab_rgb24(c, s, p);
+    // bytes per rank slot, 256-B aligned so every rank's send buffer starts aligned
+    const size_t slice = ((size_t)cap * p->width * (rgb24 ? 3u : 4u) + 255u) & ~(size_t)255u;
+    const uint32_t kflags = rgb24 ? kFlagSlabRgb24 : 0u;
     // one rank: no exchange (RRTE_FORCE_GATHER=1 still takes the gather path: tests on one GPU)
     if (c->nranks == 1 && !(c->env_force_gather && c->comm)) {
         r = launch(c, s, p, p->height, static_cast<uint32_t*>(d_full), nullptr, st);
@@ -992,25 +1015,33 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
     // slabs are a ring shared by every frame in flight, whatever stream it comes on: a frame
     // waits until the previous user of its slab has been gathered
     const int slot = (int)(c->gather_frames % rrte_ctx::kSlabs);
-    if (c->cap_slab[slot] < slice * (size_t)c->nranks) HIPCHK(c, hipDeviceSynchronize());
-    if ((r = ensure(c, c->d_slab[slot], c->cap_slab[slot], slice * (size_t)c->nranks)) != RRTE_OK) return r;
-    uint32_t* slab = c->d_slab[slot];
-    uint32_t* mine = slab + (size_t)c->rank * slice;  // in-place send slot
+    const size_t slab_words = slice * (size_t)c->nranks / 4u;
+    if (c->cap_slab[slot] < slab_words) HIPCHK(c, hipDeviceSynchronize());
+    if ((r = ensure(c, c->d_slab[slot], c->cap_slab[slot], slab_words)) != RRTE_OK) return r;
+    uint8_t* slab = reinterpret_cast<uint8_t*>(c->d_slab[slot]);
+    uint8_t* mine = slab + (size_t)c->rank * slice;  // in-place send slot
+    uint32_t* mine32 = reinterpret_cast<uint32_t*>(mine);
+    auto deinterleave = [&](hipStream_t ds) -> rrte_status {
+        if (rgb24)
+            hipLaunchKernelGGL(deinterleave_kernel<true>, dg, dim3(256), 0, ds, slab, static_cast<uint32_t*>(d_full),
+                               p->width, band, (uint32_t)c->nranks, slice);
+        else
+            hipLaunchKernelGGL(deinterleave_kernel<false>, dg, dim3(256), 0, ds, slab, static_cast<uint32_t*>(d_full),
+                               p->width, band, (uint32_t)c->nranks, slice);
+        HIPCHK(c, hipGetLastError());
+        return RRTE_OK;
+    };
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[slot], 0));
     if (!(p->flags & RRTE_FLAG_GATHER_OVERLAP)) {
         // everything on `st`: render this rank's bands into its slot, gather in place, de-interleave.
         // Gathers on one communicator must run in the same order on every rank: when frames come
         // on several streams, each waits for the previous frame's gather.
-        if ((r = launch(c, s, &pp, rows, mine, nullptr, st)) != RRTE_OK) return r;
+        if ((r = launch(c, s, &pp, rows, mine32, nullptr, st, kflags)) != RRTE_OK) return r;
         HIPCHK(c, hipEventRecord(c->ev1, st));
         if (c->gather_frames > 0)
             HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[(c->gather_frames - 1) % rrte_ctx::kSlabs], 0));
-        NCCLCHK(c, ncclGather(mine, slab, slice * 4, ncclUint8, root, c->comm, st));
-        if (c->rank == root) {
-            hipLaunchKernelGGL(deinterleave_kernel, dg, dim3(256), 0, st, slab, static_cast<uint32_t*>(d_full),
-                               p->width, p->height, band, (uint32_t)c->nranks, cap);
-            HIPCHK(c, hipGetLastError());
-        }
+        NCCLCHK(c, ncclGather(mine, slab, slice, ncclUint8, root, c->comm, st));
+        if (c->rank == root && (r = deinterleave(st)) != RRTE_OK) return r;
         HIPCHK(c, hipEventRecord(c->ev_gath[slot], st));
         ++c->gather_frames;
     } else {
@@ -1023,18 +1054,16 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
         const int lane = (int)(c->gather_frames % (uint64_t)c->ncomms);
         ncclComm_t gc = c->gcomm[lane] ? c->gcomm[lane] : c->comm;
         hipStream_t gs = c->gstream[lane];
-        if ((r = launch(c, s, &pp, rows, mine, nullptr, st)) != RRTE_OK) return r;
+        if ((r = launch(c, s, &pp, rows, mine32, nullptr, st, kflags)) != RRTE_OK) return r;
         HIPCHK(c, hipEventRecord(c->ev_rend[slot], st));
         HIPCHK(c, hipStreamWaitEvent(gs, c->ev_rend[slot], 0));
-        NCCLCHK(c, ncclGather(mine, slab, slice * 4, ncclUint8, root, gc, gs));
+        NCCLCHK(c, ncclGather(mine, slab, slice, ncclUint8, root, gc, gs));
         if (c->rank == root) {
             // frames may finish out of order across the two comm streams: the de-interleave of frame k
             // into d_full must not overtake frame k-1's (same output buffer when the caller reuses it)
             if (c->gather_frames > 0)
                 HIPCHK(c, hipStreamWaitEvent(gs, c->ev_gath[(c->gather_frames - 1) % rrte_ctx::kSlabs], 0));
-            hipLaunchKernelGGL(deinterleave_kernel, dg, dim3(256), 0, gs, slab, static_cast<uint32_t*>(d_full),
-                               p->width, p->height, band, (uint32_t)c->nranks, cap);
-            HIPCHK(c, hipGetLastError());
+            if ((r = deinterleave(gs)) != RRTE_OK) return r;
         }
         HIPCHK(c, hipEventRecord(c->ev_gath[slot], gs));
         ++c->gather_frames;

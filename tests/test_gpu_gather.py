@@ -8,19 +8,27 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from rrte_amd import LoweredScene, abi, scenes
-from rrte_amd.math import vec3
+from rrte_amd import LambertianMaterial, LoweredScene, abi, scenes
+from rrte_amd.math import Color, vec3
 from rrte_amd.renderer import Context
 
 pytestmark = pytest.mark.gpu
 
 
-def _frames(n, w=320, h=200):
+def _frames(n, w=320, h=200, alpha=None):
+    """`alpha`: None = the stock scene (every alpha byte 255: RGB24 slabs); "material" = one material
+    with albedo alpha -150 (its pixels' alpha byte 127); "spp2" = 2 samples under a background alpha
+    of 0.2 (sky pixels 178).  The last two must fall back to RGBA8 slabs."""
     out = []
     for i in range(n):
         objs, lights, cam, cfg = scenes.sdf_showcase(w, h)
         cam.transform.position = vec3(0.0 + 0.7 * i, 8.0 - 0.3 * i, 20.0)
         cam.look_at((0, 2, 0))
+        if alpha == "material":
+            objs[3].material = LambertianMaterial(Color(0.2, 0.6, 0.9, -150.0))
+        elif alpha == "spp2":
+            cfg.samples_per_pixel = 2
+            cfg.background_color = Color(0.05, 0.05, 0.08, 0.2)
         out.append((LoweredScene(objs, lights, cam), cfg.lower()))
     return out
 
@@ -29,11 +37,23 @@ def _frames(n, w=320, h=200):
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
 def test_gather_path_matches_plain_render(overlap, jit, comms, monkeypatch):
+    _check_gather(overlap, jit, comms, monkeypatch, None)
+
+
+@pytest.mark.parametrize("alpha,rgb24", [(None, "0"), ("material", "1"), ("spp2", "1")])
+def test_gather_slab_formats(alpha, rgb24, monkeypatch):
+    """RGBA8 slabs when forced (RRTE_GATHER_RGB24=0) or when some alpha byte is not 255; every
+    frame still equal to the plain render, alpha bytes included."""
+    monkeypatch.setenv("RRTE_GATHER_RGB24", rgb24)
+    _check_gather(True, abi.JIT_ON, "1", monkeypatch, alpha)
+
+
+def _check_gather(overlap, jit, comms, monkeypatch, alpha):
     import torch
 
     monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
     monkeypatch.setenv("RRTE_GATHER_COMMS", comms)
-    frames = _frames(7)
+    frames = _frames(7, alpha=alpha)
     w, h = frames[0][1].width, frames[0][1].height
     ref = Context(0, jit=jit)
     want = []
@@ -61,6 +81,8 @@ def test_gather_path_matches_plain_render(overlap, jit, comms, monkeypatch):
     for i, o in enumerate(outs):
         got = o.cpu().numpy().view(np.uint8)
         assert np.array_equal(got, want[i]), f"frame {i}: {(got != want[i]).sum()} bytes differ"
+    if alpha is not None:  # the scene really has alpha bytes below 255
+        assert (want[0].reshape(-1, 4)[:, 3] < 255).any()
     # blocking variant to host memory
     buf = np.zeros(w * h * 4, dtype=np.uint8)
     sc, prm = frames[2]
