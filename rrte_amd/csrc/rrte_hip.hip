@@ -1016,8 +1016,13 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
     // waits until the previous user of its slab has been gathered
     const int slot = (int)(c->gather_frames % rrte_ctx::kSlabs);
     const size_t slab_words = slice * (size_t)c->nranks / 4u;
-    if (c->cap_slab[slot] < slab_words) HIPCHK(c, hipDeviceSynchronize());
-    if ((r = ensure(c, c->d_slab[slot], c->cap_slab[slot], slab_words)) != RRTE_OK) return r;
+    if (c->cap_slab[slot] < slab_words) {
+        // (re)size the whole ring at once: one device synchronisation (no slab may be freed under an
+        // in-flight gather) instead of one per slot spread over the first kSlabs frames
+        HIPCHK(c, hipDeviceSynchronize());
+        for (int i = 0; i < rrte_ctx::kSlabs; ++i)
+            if ((r = ensure(c, c->d_slab[i], c->cap_slab[i], slab_words)) != RRTE_OK) return r;
+    }
     uint8_t* slab = reinterpret_cast<uint8_t*>(c->d_slab[slot]);
     uint8_t* mine = slab + (size_t)c->rank * slice;  // in-place send slot
     uint32_t* mine32 = reinterpret_cast<uint32_t*>(mine);
