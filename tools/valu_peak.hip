@@ -66,6 +66,12 @@ SK(k_cmpsel32, "v_cmp_lt_f32 vcc, %1, %0\n\tv_cndmask_b32 %0, %0, %1, vcc", "vcc
 SK(k_cnd64s, "v_cndmask_b32_e64 %0, %1, %0, s[20:21]", "s20", "s21")
 // e64 select reading VCC
 SK(k_cnd64v, "v_cndmask_b32_e64 %0, %1, %0, vcc", "vcc")
+// integer ops of the value-noise lattice hash (device_scene.hpp lattice)
+SK(k_mullo, "v_mul_lo_u32 %0, %1, %0", "memory")
+SK(k_mul24, "v_mul_u32_u24 %0, %1, %0", "memory")
+SK(k_xor, "v_xor_b32 %0, %1, %0", "memory")
+SK(k_lshr, "v_lshrrev_b32 %0, 16, %0", "memory")
+SK(k_cvt, "v_cvt_f32_u32 %0, %0", "memory")
 KERNEL(k_pkfma, f2, "v_pk_fma_f32 %0, %1, %2, %0")
 KERNEL(k_pkadd, f2, "v_pk_add_f32 %0, %1, %0")
 KERNEL(k_pkmul, f2, "v_pk_mul_f32 %0, %1, %0")
@@ -121,6 +127,11 @@ int main(int argc, char** argv) {
     run("v_cmp_e32+v_cndmask_e32 vcc (pair, counted as 1)", k_cmpsel32, 1.0f, 0.0f, blocks, buf, 0);
     run("v_cndmask_b32_e64 s[20:21]", k_cnd64s, 1.0f, 0.0f, blocks, buf, 0);
     run("v_cndmask_b32_e64 vcc", k_cnd64v, 1.0f, 0.0f, blocks, buf, 0);
+    run("v_mul_lo_u32", k_mullo, 1.0f, 0.0f, blocks, buf, 0);
+    run("v_mul_u32_u24", k_mul24, 1.0f, 0.0f, blocks, buf, 0);
+    run("v_xor_b32", k_xor, 1.0f, 2.0f, blocks, buf, 0);
+    run("v_lshrrev_b32", k_lshr, 1.0f, 0.0f, blocks, buf, 0);
+    run("v_cvt_f32_u32", k_cvt, 1.0f, 0.0f, blocks, buf, 0);
     run("v_pk_fma_f32", k_pkfma, m2, c2, blocks, buf, 4);
     run("v_pk_add_f32", k_pkadd, c2, c2, blocks, buf, 2);
     run("v_pk_mul_f32", k_pkmul, m2, c2, blocks, buf, 2);
