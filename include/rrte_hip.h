@@ -317,9 +317,12 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* scene, int mode, char* log, 
  *   RRTE_FPCHECK_DIV: a/b for every significand of a in [1, 2) and every b = 1 + k*2^-23,
  *                     k in [lo, hi) (hi <= 2^23), with y = rcp_rn(b).  Synchronous. */
 /*   RRTE_FPCHECK_SQRT_HW: control -- the bare v_sqrt_f32 against the correctly rounded sqrt
- *                         (the sweep must find its 1-ulp errors). */
+ *                         (the sweep must find its 1-ulp errors).
+ *   RRTE_FPCHECK_GAMMA_U8: every f32 bit pattern in [lo, hi): the kernels' gamma-2.2 byte
+ *                          (ray_kernels.hpp gamma22_u8) against to_u8(clamp(powf(c, 1/2.2))). */
 typedef enum rrte_fpcheck {
-    RRTE_FPCHECK_SQRT = 0, RRTE_FPCHECK_RCP = 1, RRTE_FPCHECK_DIV = 2, RRTE_FPCHECK_SQRT_HW = 3
+    RRTE_FPCHECK_SQRT = 0, RRTE_FPCHECK_RCP = 1, RRTE_FPCHECK_DIV = 2, RRTE_FPCHECK_SQRT_HW = 3,
+    RRTE_FPCHECK_GAMMA_U8 = 4
 } rrte_fpcheck;
 rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uint64_t* mismatches);
 /* Diagnostic (host only): the CSG early-out decoration the renderer applies to one SDF program

@@ -35,7 +35,7 @@ SDF_POP_POINT = 96
 SDF_MAX_STACK, SDF_MAX_POINT_STACK, SDF_MAX_OCTAVES = 8, 4, 8
 UNIQUE_ID_BYTES = 128
 JIT_OFF, JIT_ON, JIT_AUTO = 0, 1, 2
-FPCHECK_SQRT, FPCHECK_RCP, FPCHECK_DIV, FPCHECK_SQRT_HW = 0, 1, 2, 3
+FPCHECK_SQRT, FPCHECK_RCP, FPCHECK_DIV, FPCHECK_SQRT_HW, FPCHECK_GAMMA_U8 = 0, 1, 2, 3, 4
 
 
 # --------------------------------------------------------------- structs

@@ -1327,6 +1327,25 @@ __device__ __forceinline__ float rclamp(float x) {
     return x;
 }
 
+// One channel of the reference's fixed to_gamma(2.2) -> clamp -> truncating u8 (raytracer.rs:79-85,
+// color.rs:58-65) without powf in the common case.  The compiler's powf is a ~100-instruction
+// double-float sequence, a tenth of the headline kernel with three per pixel.  y = exp2(log2(c)/2.2)
+// from v_log_f32 / v_exp_f32 is within a few ulp of it; RN(p*255) and the clamp are monotone in p,
+// so when y(1 - m) and y(1 + m) quantise to the same byte every p in between -- powf's result
+// included -- does too, and that byte is the answer.  Lanes near a byte boundary, +inf and -inf
+// take powf.  Bit-identical to to_u8(rclamp(powf(c, RN(1/2.2)))) for all 2^32 inputs
+// (rrte_hip_fpcheck RRTE_FPCHECK_GAMMA_U8, tests/test_gpu_fpexact.py).
+constexpr float kInvGamma22 = 1.0f / 2.2f;
+constexpr float kGammaMargin = 0x1p-20f;  // relative, ~8 ulp
+__device__ __forceinline__ uint32_t gamma22_u8(float c) {
+    const float y = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(c) * kInvGamma22);
+    const float m = y * kGammaMargin;
+    const uint32_t a = to_u8(rclamp(y - m)), b = to_u8(rclamp(y + m));
+    // c = -inf: log2 gives NaN (byte 0) but powf(-inf, 1/2.2) = +inf (byte 255)
+    if (__builtin_expect(a == b && c != -kInf, 1)) return a;
+    return to_u8(rclamp(powf(c, kInvGamma22)));
+}
+
 // Map this launch's local row to the image row (band interleave, §8e).
 __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
     if (kp.band_rows == 0) return r;
@@ -1414,11 +1433,20 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
         acc.b = acc.b * kp.inv_spp;
         acc.a = acc.a * kp.inv_spp;
         const float ig = kp.inv_gamma;
-        float gr = rclamp(powf(acc.r, ig)), gg = rclamp(powf(acc.g, ig)), gb = rclamp(powf(acc.b, ig));
-        float ga = rclamp(acc.a);
+        const float ga = rclamp(acc.a);
         const size_t o = (size_t)lr * kp.width + x;  // packed local rows
+        // the parity float buffer (or a gamma other than the reference's 2.2) needs powf itself
+        const bool exact_pow = out_f32 || ig != kInvGamma22;
+        float gr = 0.0f, gg = 0.0f, gb = 0.0f;
+        if (exact_pow) {
+            gr = rclamp(powf(acc.r, ig));
+            gg = rclamp(powf(acc.g, ig));
+            gb = rclamp(powf(acc.b, ig));
+        }
         if (out_rgba8) {
-            const uint32_t px = to_u8(gr) | (to_u8(gg) << 8) | (to_u8(gb) << 16) | (to_u8(ga) << 24);
+            const uint32_t px = exact_pow ? (to_u8(gr) | (to_u8(gg) << 8) | (to_u8(gb) << 16) | (to_u8(ga) << 24))
+                                          : (gamma22_u8(acc.r) | (gamma22_u8(acc.g) << 8) | (gamma22_u8(acc.b) << 16) |
+                                             (to_u8(ga) << 24));
             if (kp.flags & kFlagSlabRgb24) {  // gather slab, alpha proven 255: 3 bytes per pixel
                 uint8_t* b = reinterpret_cast<uint8_t*>(out_rgba8) + 3u * o;
                 b[0] = (uint8_t)px;

@@ -703,6 +703,7 @@ __global__ __launch_bounds__(256) void fpcheck_unary_kernel(int kind, uint64_t x
         bool bad;
         if (kind == RRTE_FPCHECK_SQRT) bad = !fp_same(sqrt_rn(x), __builtin_sqrtf(x));
         else if (kind == RRTE_FPCHECK_RCP) bad = !fp_same(rcp_rn(x), 1.0f / x);
+        else if (kind == RRTE_FPCHECK_GAMMA_U8) bad = gamma22_u8(x) != to_u8(rclamp(powf(x, kInvGamma22)));
         else bad = !fp_same(__builtin_amdgcn_sqrtf(x), __builtin_sqrtf(x));
         fp_count(in && bad, out);
     }
@@ -891,7 +892,7 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
 }
 
 rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uint64_t* mismatches) {
-    if (!mismatches || kind < RRTE_FPCHECK_SQRT || kind > RRTE_FPCHECK_SQRT_HW || lo > hi ||
+    if (!mismatches || kind < RRTE_FPCHECK_SQRT || kind > RRTE_FPCHECK_GAMMA_U8 || lo > hi ||
         hi > (kind == RRTE_FPCHECK_DIV ? (1ull << 23) : (1ull << 32)))
         return RRTE_INVALID_ARG;
     if (hipSetDevice(device) != hipSuccess) return RRTE_HIP_ERROR;

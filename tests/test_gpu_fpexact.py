@@ -36,6 +36,12 @@ def test_rcp_rn_all_inputs():
     assert _check(abi.FPCHECK_RCP, 0, 1 << 32) == 0
 
 
+def test_gamma_byte_all_inputs():
+    """The frame's gamma-2.2 byte from v_log_f32 / v_exp_f32 with a powf fallback near byte
+    boundaries equals to_u8(clamp(powf(c, 1/2.2))) for every f32 c."""
+    assert _check(abi.FPCHECK_GAMMA_U8, 0, 1 << 32) == 0
+
+
 @pytest.mark.parametrize("lo,hi", [(0, 1 << 12), ((1 << 23) - (1 << 12), 1 << 23)]
                          + [(k << 20, (k << 20) + (1 << 17)) for k in range(8)])
 def test_constant_divisor_step(lo, hi):
