@@ -21,10 +21,11 @@ from pathlib import Path
 import numpy as np
 
 # Frames in flight need their streams on distinct hardware queues; HIP's default of 4 per
-# process is shared with torch's and the library's own streams (measured, tools/inflight_sweep.sh:
-# an N=8 rank's frame takes 40 us with 4 queues / 4 frames, 24 us with 8 / 4, 20 us with 16 / 8).
+# process is shared with torch's and the library's own streams (measured, tools/inflight_sweep.sh and
+# tools/inflight_q_sweep.sh: an N=8 rank's frame takes 40 us with 4 queues / 4 frames, 24 us with
+# 8 / 4, 17 us with 16 / 8, 14 us with 32 / 12; one GPU's whole frame is 95.5 us at all of the last three).
 # Must be set before HIP starts.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "32")
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -39,7 +40,7 @@ VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (packed)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)  # 0.1 ms frames: 200 keep the ramp/drain under 5 %
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scene", default="sdf-showcase", choices=sorted(scenes.SCENES))
     ap.add_argument("--width", type=int, default=1920)
@@ -52,7 +53,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stock", action="store_true", help="skip the stock-config secondary measurement")
-    ap.add_argument("--inflight", type=int, default=8,
+    ap.add_argument("--inflight", type=int, default=12,
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
                          "so one frame's tail overlaps the next frame's start (1 = strictly one after another)")
     ap.add_argument("--no-overlap", action="store_true",
