@@ -357,12 +357,23 @@ struct SdfStaticProgram {
     }
 };
 
+// Exact "ray leaves the sphere" early-out for any-hit (shadow) rays: origin outside the sphere
+// (cc = |oc|^2 - r^2 > 0) moving away from its centre (hb = oc.d > 0), |d|^2 >= 1/4, t_min >= 2^-57.
+// Then the full test finds nothing in [t_min, t_max]: disc = RN(RN(hb^2) - RN(a cc)) <= RN(hb^2), so
+// sq = RN(sqrt(disc)) <= RN(sqrt(RN(hb^2))), which is hb when hb >= 2^-60 (fl(sqrt(fl(x*x))) = |x| in
+// binary f32 with round-to-nearest, no under/overflow) and <= 2^-60 otherwise; hence -hb + sq <= 2^-60,
+// both roots (-hb -/+ sq)/a are <= 2^-58 < t_min, and the sphere / bounding-sphere test rejects.
+// Skips the sqrt and divides of, e.g., every shadow ray's test against the ground sphere.
+__device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float t_min) {
+    return hb > 0.0f && cc > 0.0f && a >= 0.25f && t_min >= 0x1p-57f;
+}
+
 // SDFObject::intersect, search part -- sphere tracing inside the object's
 // bounding sphere (build-defined).  Only t is produced here;
 // the closest-hit search keeps (t, object) and the hit attributes are
 // computed once for the winner.  The per-lane trip count diverges; the wave
 // leaves the loop when its EXEC mask drains.
-template <class EVAL>
+template <class EVAL, bool ANY = false>
 __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
                                           float& t_hit) {
     f3 bc = V(pr.p[0], pr.p[1], pr.p[2]);
@@ -370,6 +381,9 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     f3 oc = vsub(r.o, bc);
     float b = vdot(oc, r.d);
     float cc = vdot(oc, oc) - br * br;
+    // the bound test below has no divide (roots -b -/+ sq): leaves_sphere's argument with a = 1, which
+    // leaves tend = mn(t_max, -b + sq) <= 2^-60 < t_min <= t unless t_max is NaN (tend NaN marches on)
+    if (ANY && t_max == t_max && leaves_sphere(b, cc, 1.0f, t_min)) return false;
     float disc = b * b - cc;
     if (disc < 0.0f) return false;
     float sq = sqrt_rn(disc);
@@ -425,7 +439,7 @@ __device__ __forceinline__ void local_ray(const DPrim& pr, const Ray& r, Ray& lr
 // ----------------------------------------------------- analytic intersectors
 // SceneObject::intersect for the seven primitive kinds (primitives.rs:57-725).
 // t is always written to out.t; point/normal only matter when NEED_HIT.
-template <bool NEED_HIT>
+template <bool NEED_HIT, bool ANY = false>
 __device__ __forceinline__ bool isect_sphere(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:57-81
     f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
     float rad = pr.p[3];
@@ -433,6 +447,7 @@ __device__ __forceinline__ bool isect_sphere(const DPrim& pr, const Ray& r, floa
     float a = vlen2(r.d);
     float hb = vdot(oc, r.d);
     float cc = vlen2(oc) - rad * rad;
+    if (ANY && leaves_sphere(hb, cc, a, t_min)) return false;
     float disc = hb * hb - a * cc;
     if (disc < 0.0f) return false;
     float sq = sqrt_rn(disc);
@@ -639,11 +654,11 @@ __device__ __forceinline__ bool isect_capsule(const DPrim& pr, const Ray& r, flo
     return found;
 }
 
-template <bool NEED_HIT, class EVAL>
+template <bool NEED_HIT, class EVAL, bool ANY = false>
 __device__ __forceinline__ bool isect_sdf(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
                                           Hit& out) {
     float t;
-    if (!sdf_march(pr, eval, r, t_min, t_max, t)) return false;
+    if (!sdf_march<EVAL, ANY>(pr, eval, r, t_min, t_max, t)) return false;
     if (NEED_HIT) sdf_hit_attributes(eval, r, t, out);
     else out.t = t;
     return true;
@@ -791,7 +806,7 @@ __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray&
                                              Hit& out) {
     const DPrim& pr = sc.prims[i];
     switch (pr.kind) {
-    case RRTE_PRIM_SPHERE: return isect_sphere<NEED_HIT>(pr, r, t_min, t_max, out);
+    case RRTE_PRIM_SPHERE: return isect_sphere<NEED_HIT, ANY>(pr, r, t_min, t_max, out);
     case RRTE_PRIM_PLANE: return isect_plane<NEED_HIT>(pr, r, t_min, t_max, out);
     case RRTE_PRIM_TRIANGLE: return isect_triangle<NEED_HIT>(pr, r, t_min, t_max, out);
     case RRTE_PRIM_CUBE: return isect_cube<NEED_HIT>(pr, r, t_min, t_max, out);
@@ -799,7 +814,8 @@ __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray&
     case RRTE_PRIM_CONE: return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
     case RRTE_PRIM_CAPSULE: return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
     case RRTE_PRIM_SDF:
-        return isect_sdf<NEED_HIT>(pr, SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t_min, t_max, out);
+        return isect_sdf<NEED_HIT, SdfProgram, ANY>(pr, SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t_min,
+                                                    t_max, out);
     case RRTE_PRIM_MESH: return isect_mesh<ANY>(pr, sc.mesh, r, t_min, t_max, out);
     default: return false;
     }
@@ -811,7 +827,7 @@ template <bool NEED_HIT, class S, uint32_t I, bool ANY = false>
 __device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, float t_min, float t_max, Hit& out) {
     constexpr DPrim pr = S::prims[I];
     constexpr uint32_t kind = pr.kind;
-    if constexpr (kind == RRTE_PRIM_SPHERE) return isect_sphere<NEED_HIT>(pr, r, t_min, t_max, out);
+    if constexpr (kind == RRTE_PRIM_SPHERE) return isect_sphere<NEED_HIT, ANY>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_PLANE) return isect_plane<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_TRIANGLE) return isect_triangle<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_CUBE) return isect_cube<NEED_HIT>(pr, r, t_min, t_max, out);
@@ -819,7 +835,8 @@ __device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, f
     else if constexpr (kind == RRTE_PRIM_CONE) return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_CAPSULE) return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_SDF)
-        return isect_sdf<NEED_HIT>(pr, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t_min, t_max, out);
+        return isect_sdf<NEED_HIT, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>, ANY>(
+            pr, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_MESH) return isect_mesh<ANY>(pr, sc.mesh, r, t_min, t_max, out);
     else return false;
 }
