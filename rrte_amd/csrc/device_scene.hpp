@@ -76,6 +76,12 @@ struct KParams {
     float ortho_l, ortho_r, ortho_b, ortho_t;
     float cam_xf[12];
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
+    // Camera-ray tile culling (perspective frames, objects [0, tile_n), tile_n <= 32): object i's
+    // bounding sphere projects inside the 16x16-pixel block rectangle tile_rect[i] = bx0 | bx1 << 8 |
+    // by0 << 16 | by1 << 24 (inclusive, conservative); a workgroup outside it cannot hit object i with
+    // a camera ray.  tile_cull == 0: off.
+    uint32_t tile_cull, tile_n;
+    uint32_t tile_rect[32];
 };
 
 // Internal KParams::flags bit (never in the public rrte_render_params::flags): the launch writes

@@ -845,13 +845,18 @@ __device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, f
 // earlier object on ties; analytic objects get t_max = INFINITY as in the
 // reference, SDF objects march only up to the current closest hit.  The
 // search carries only (t, object); attributes are produced afterwards.
+// `pmask` (camera rays): bit i clear = object i's bounding sphere lies outside this workgroup's
+// pixel block (KParams::tile_rect), so no lane can hit it and its test is skipped (exact: the
+// skipped test would have missed on every lane).
 template <class S>
-__device__ __forceinline__ int closest_t(const S& sc, const Ray& r, float t_min, float& best_t, uint32_t& best_sub) {
+__device__ __forceinline__ int closest_t(const S& sc, const Ray& r, float t_min, float& best_t, uint32_t& best_sub,
+                                         uint32_t pmask = ~0u) {
     int idx = -1;
     best_t = kInf;
     best_sub = 0u;
     for_each_prim(sc, [&](auto ii) {
         const uint32_t i = ii;
+        if (i < 32u && !((pmask >> i) & 1u)) return;
         Hit h;
         h.sub = 0u;
         float tmax = (prim_at(sc, ii).kind == RRTE_PRIM_SDF && idx >= 0) ? best_t : kInf;
@@ -915,10 +920,10 @@ __device__ __forceinline__ void hit_attributes(const S& sc, const Ray& r, float 
 }
 
 template <class S>
-__device__ __forceinline__ int closest_hit(const S& sc, const Ray& r, float t_min, Hit& best) {
+__device__ __forceinline__ int closest_hit(const S& sc, const Ray& r, float t_min, Hit& best, uint32_t pmask = ~0u) {
     float t;
     uint32_t sub;
-    int idx = closest_t(sc, r, t_min, t, sub);
+    int idx = closest_t(sc, r, t_min, t, sub, pmask);
     hit_attributes(sc, r, t_min, idx, t, sub, best);
     return idx;
 }
@@ -1191,11 +1196,13 @@ __device__ __forceinline__ void path_begin(PathState& ps, const Ray& r) {
     ps.depth = 0;
 }
 
-// One bounce of ray_color (kp.max_depth >= 1); true when the path has ended.
+// One bounce of ray_color (kp.max_depth >= 1); true when the path has ended.  pmask: camera-ray
+// tile culling mask (only for the camera ray, ~0u otherwise).
 template <class S>
-__device__ __forceinline__ bool path_step(const S& sc, const KParams& kp, PathState& ps, uint32_t& st) {
+__device__ __forceinline__ bool path_step(const S& sc, const KParams& kp, PathState& ps, uint32_t& st,
+                                          uint32_t pmask = ~0u) {
     Hit h;
-    const int idx = closest_hit(sc, ps.r, kp.t_min, h);
+    const int idx = closest_hit(sc, ps.r, kp.t_min, h, pmask);
     const uint32_t depth = ps.depth;
     if (idx < 0) {
         if (depth == 0) {
@@ -1244,12 +1251,13 @@ __device__ __forceinline__ bool path_step(const S& sc, const KParams& kp, PathSt
 // The whole path of one camera ray.  SINGLE (scene-specialised straight-line kernels): one
 // bounce only (max_depth <= 1).
 template <class S, bool SINGLE>
-__device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray r, uint32_t& st) {
+__device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray r, uint32_t& st,
+                                             uint32_t pmask = ~0u) {
     PathState ps;
     path_begin(ps, r);
     if (kp.max_depth == 0) return ps.out;
     if constexpr (SINGLE) {
-        path_step(sc, kp, ps, st);
+        path_step(sc, kp, ps, st, pmask);
     } else {
 #pragma unroll 1
         while (!path_step(sc, kp, ps, st)) {
@@ -1263,11 +1271,11 @@ __device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray
 // CULL the hit-point bound and the per-light shadow culls are wave reductions.
 template <class S, bool CULL>
 __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, const Cull& cl, const Ray& r, bool live,
-                                             uint32_t& nshadow) {
+                                             uint32_t& nshadow, uint32_t pmask = ~0u) {
     Col out{0.0f, 0.0f, 0.0f, 1.0f};
     if (kp.max_depth == 0) return out;
     Hit h;
-    const int idx = closest_hit(sc, r, live ? kp.t_min : kInf, h);  // idle lanes find nothing
+    const int idx = closest_hit(sc, r, live ? kp.t_min : kInf, h, pmask);  // idle lanes find nothing
     const DMaterial* m = idx >= 0 ? material_of(sc, idx) : nullptr;
     const bool hit = m != nullptr;
     if (idx < 0) out = Col{kp.bg[0], kp.bg[1], kp.bg[2], kp.bg[3]};
@@ -1370,6 +1378,21 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
     return (b * kp.nranks + kp.rank) * kp.band_rows + w;
 }
 
+// Camera-ray tile culling mask of this workgroup's 16x16-pixel block (KParams::tile_rect): wave-
+// uniform, scalar ALU only.  The host enables it only when a block's 16 local rows are 16
+// consecutive image rows (no band mapping, or bands of a multiple of 16 rows).
+__device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp) {
+    if (!kp.tile_cull) return ~0u;
+    const uint32_t bx = blockIdx.x, by = image_row(kp, blockIdx.y * 16u) >> 4;
+    uint32_t m = kp.tile_n < 32u ? (~0u << kp.tile_n) : 0u;  // objects past the table: never culled
+#pragma unroll 1
+    for (uint32_t i = 0; i < kp.tile_n; ++i) {
+        const uint32_t t = kp.tile_rect[i];
+        if (bx >= (t & 255u) && bx <= ((t >> 8) & 255u) && by >= ((t >> 16) & 255u) && by <= (t >> 24)) m |= 1u << i;
+    }
+    return __builtin_amdgcn_readfirstlane(m);
+}
+
 // One lane per pixel; wave = 8x8 tile, workgroup = 16x16 pixels.  Every lane
 // of a wave runs the sample loop (lanes past the image edge are idle but
 // present) so the culling reductions see converged waves.  CULL selects the
@@ -1388,6 +1411,7 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     uint32_t nshadow = 0;
     Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
     const uint32_t nsamples = SINGLE ? 1u : kp.spp;
+    const uint32_t pmask = camera_tile_mask(kp);
     // camera ray of sample s (raytracer.rs:66-70): per-(pixel, sample) RNG stream, jitter, generate_ray
     auto camera_ray = [&](uint32_t s, uint32_t& st) {
         st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
@@ -1437,9 +1461,9 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
             Ray r = camera_ray(s, st);
             Col c{0.0f, 0.0f, 0.0f, 1.0f};
             if (MODE == RRTE_MODE_LAMBERT_SHADOW) {
-                c = shade_lambert<S, CULL>(sc, kp, cl, r, live, nshadow);
+                c = shade_lambert<S, CULL>(sc, kp, cl, r, live, nshadow, pmask);
             } else if (live) {
-                c = ray_color_ref<S, SINGLE>(sc, kp, r, st);
+                c = ray_color_ref<S, SINGLE>(sc, kp, r, st, SINGLE ? pmask : ~0u);
             }
             accumulate(c);
         }

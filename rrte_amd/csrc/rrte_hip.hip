@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -79,6 +80,7 @@ struct rrte_ctx {
     // environment switches, read once at rrte_hip_create (diagnostics / A-B runs / tests)
     uint32_t env_debug = 0;       // RRTE_DEBUG ablation bits
     int env_cull = -1;            // RRTE_CULL: -1 unset, 0 off, 1 on
+    bool env_tile_cull = true;    // RRTE_TILE_CULL=0: no camera-ray tile culling (A/B, tests)
     bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
     bool env_gather_rgba = false;   // RRTE_GATHER_RGB24=0: gather slabs always RGBA8
     uint32_t env_guard_leaves = 2;  // RRTE_CSG_GUARDS: 0 = off, N = smallest guarded operand (leaves)
@@ -87,6 +89,7 @@ struct rrte_ctx {
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, valid; JitKernel* k; } jit_last{};
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
     std::vector<DPrim> h_prims;                  // host copy of the lowered scene (JIT source)
+    std::vector<float4> h_bounds;                // host copy of the per-object culling spheres
     std::vector<DMaterial> h_mats;
     std::vector<DLight> h_lights;
     std::vector<rrte_sdf_node> h_nodes;
@@ -446,6 +449,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     *upload_ms = ms;
     c->mesh_view = MeshView{c->d_mesh_nodes, c->d_mesh_tris, c->d_mesh_norms, c->d_mesh_perm};
     c->h_prims = prims;
+    c->h_bounds = bounds;
     c->h_mats = mats;
     c->h_lights = lights;
     c->h_nodes = std::move(nodes);
@@ -498,6 +502,81 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     to_affine12(m, k.cam_xf);
     k.debug = c->env_debug;  // RRTE_DEBUG ablation bits (profiling only)
     return k;
+}
+
+// Camera-ray tile culling (KParams::tile_rect, ray_kernels.hpp camera_tile_mask), perspective frames:
+// for each of the first 32 objects, the 16x16-pixel blocks whose camera rays can reach its culling
+// sphere (the conservative bound shadow culling uses: centre, radius).  In camera space a ray
+// direction (x, y, -1) that meets the sphere projects, in the xz plane, onto a line through the eye
+// that meets the sphere's disc there, so x lies between the tangents of that disc (likewise y in the
+// yz plane).  Double precision, then 2 pixels of margin per side -- orders of magnitude above the f32
+// error of the device's ray directions (~1e-6 of the field of view) and of random jitter's extent
+// (inside the pixel).  A sphere that contains the eye or reaches the plane z = 0 keeps the whole
+// frame.  Bit-identical results by construction: a skipped test is one every lane would miss
+// (tests/test_gpu_parity.py test_camera_tile_culling_is_exact).
+void fill_tile_rects(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& k) {
+    k.tile_cull = 0;
+    const uint32_t nbx = (p->width + 15) / 16, nby = (p->height + 15) / 16;
+    if (!c->env_tile_cull || s->camera.projection != RRTE_PERSPECTIVE || nbx > 256 || nby > 256 ||
+        (k.band_rows != 0 && k.band_rows % 16 != 0) || c->h_bounds.size() < s->num_prims)
+        return;
+    const rrte_camera& cam = s->camera;
+    double q[4] = {cam.rotation[0], cam.rotation[1], cam.rotation[2], cam.rotation[3]};
+    const double qn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    if (!(qn > 0.0) || !std::isfinite(qn)) return;
+    for (double& v : q) v /= qn;
+    const double hh = std::tan(0.5 * (double)cam.fov), hw = (double)cam.aspect_ratio * hh;
+    if (!(hh > 0.0) || !(hw > 0.0) || !std::isfinite(hh) || !std::isfinite(hw)) return;
+    // world -> camera: the inverse rotation (conjugate quaternion) of v - position
+    auto to_cam = [&](const double v[3], double out[3]) {
+        const double bx = -q[0], by = -q[1], bz = -q[2], w = q[3];
+        const double vb = v[0] * bx + v[1] * by + v[2] * bz, k0 = w * w - (bx * bx + by * by + bz * bz);
+        const double cx = by * v[2] - bz * v[1], cy = bz * v[0] - bx * v[2], cz = bx * v[1] - by * v[0];
+        out[0] = v[0] * k0 + 2.0 * bx * vb + 2.0 * w * cx;
+        out[1] = v[1] * k0 + 2.0 * by * vb + 2.0 * w * cy;
+        out[2] = v[2] * k0 + 2.0 * bz * vb + 2.0 * w * cz;
+    };
+    const uint32_t n = s->num_prims < 32u ? s->num_prims : 32u;
+    const double margin = 2.0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const float4 b = c->h_bounds[i];
+        uint32_t rect = 0u | ((nbx - 1) << 8) | (0u << 16) | ((nby - 1) << 24);  // whole frame
+        const double R = (double)b.w;
+        const double w[3] = {(double)b.x - cam.position[0], (double)b.y - cam.position[1], (double)b.z - cam.position[2]};
+        double v[3];
+        to_cam(w, v);
+        const bool finite = std::isfinite(R) && std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]);
+        if (finite && R >= 0.0 && v[2] < -R * 1.001 - 1e-6) {  // entirely in front of the eye (z < 0)
+            // tangent slopes of the disc (centre (c, -d), radius R, d > R) seen from the origin
+            auto range = [&](double cc, double& lo, double& hi) {
+                const double d = -v[2], D = std::sqrt(cc * cc + d * d);
+                const double alpha = std::atan2(cc, d), beta = std::asin(std::min(1.0, R / D));
+                lo = std::tan(alpha - beta);
+                hi = std::tan(alpha + beta);
+            };
+            double xl, xh, yl, yh;
+            range(v[0], xl, xh);
+            range(v[1], yl, yh);
+            // ndc_x = x / hw, pixel x = (ndc_x + 1) W / 2 - 1/2;  ndc_y = y / hh, pixel y = (1 - ndc_y) H / 2 - 1/2
+            const double W = p->width, H = p->height;
+            const double px0 = (xl / hw + 1.0) * W * 0.5 - 0.5 - margin, px1 = (xh / hw + 1.0) * W * 0.5 - 0.5 + margin;
+            const double py0 = (1.0 - yh / hh) * H * 0.5 - 0.5 - margin, py1 = (1.0 - yl / hh) * H * 0.5 - 0.5 + margin;
+            if (std::isfinite(px0) && std::isfinite(px1) && std::isfinite(py0) && std::isfinite(py1)) {
+                if (px1 < 0.0 || py1 < 0.0 || px0 > W - 1.0 || py0 > H - 1.0) {
+                    rect = 0xFFu | (0xFFu << 16);  // bx0 = 255 > bx1 = 0: no block (block indices <= 255)
+                } else {
+                    auto blk = [](double px, uint32_t nb) {
+                        const double b = std::floor(px / 16.0);
+                        return (uint32_t)std::min<double>(std::max<double>(b, 0.0), (double)(nb - 1));
+                    };
+                    rect = blk(px0, nbx) | (blk(px1, nbx) << 8) | (blk(py0, nby) << 16) | (blk(py1, nby) << 24);
+                }
+            }
+        }
+        k.tile_rect[i] = rect;
+    }
+    k.tile_n = n;
+    k.tile_cull = 1;
 }
 
 uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank) {
@@ -614,6 +693,7 @@ rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params
     // single-sample, single-bounce frames get the straight-line specialisation (SINGLE); others the
     // specialisation with runtime sample / bounce loops
     const bool single = p->samples_per_pixel == 1 && (p->mode == RRTE_MODE_LAMBERT_SHADOW || p->max_depth <= 1);
+    fill_tile_rects(c, s, p, k);
     JitKernel* jk = jit_kernel_for(c, (int)p->mode, cull, single);
     c->stats.jit_active = jk ? 1u : 0u;
     if (jk) {
@@ -733,6 +813,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* j = getenv("RRTE_JIT")) c->jit_mode = (int)strtol(j, nullptr, 0);
     if (const char* d = getenv("RRTE_DEBUG")) c->env_debug = (uint32_t)strtoul(d, nullptr, 0);
     c->env_cull = env_cull_setting();
+    if (const char* t = getenv("RRTE_TILE_CULL")) c->env_tile_cull = t[0] != '0';
     if (const char* g = getenv("RRTE_FORCE_GATHER")) c->env_force_gather = g[0] == '1';
     if (const char* g = getenv("RRTE_GATHER_RGB24")) c->env_gather_rgba = g[0] == '0';
     c->env_guard_leaves = env_guard_setting();

@@ -215,6 +215,35 @@ def test_camera_motion_on_one_specialised_kernel(name):
     compare(objs, lights, oc, cfg, jit=abi.JIT_ON)
 
 
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+@pytest.mark.parametrize("name", ["sdf-showcase", "sdf-showcase-literal", "advanced-demo", "basic-demo"])
+def test_camera_tile_culling_is_exact(name, jit, monkeypatch):
+    """Camera-ray tile culling (KParams::tile_rect: a 16x16 block skips objects whose bounding sphere
+    projects outside it) never changes a bit: off and on give identical linear images and shadow-ray
+    counts for poses with objects off screen, at the frame edge, close to the eye and behind it,
+    a wide and a narrow field of view, odd frame sizes and random jitter."""
+    poses = [((0.0, 8.0, 20.0), (0.0, 2.0, 0.0), 45.0), ((-11.0, 2.5, -3.0), (4.0, 2.0, -8.0), 80.0),
+             ((-8.0, 2.0, 1.5), (-8.0, 2.0, -8.0), 30.0), ((3.0, 1.0, 3.0), (12.0, 2.0, 0.0), 100.0),
+             ((0.0, 3.0, 0.0), (0.0, 2.0, 10.0), 60.0), ((14.0, 6.0, 9.0), (-2.0, 1.0, -4.0), 20.0)]
+    rts = {}
+    for tc in ("0", "1"):  # the switch is read when a context is created
+        monkeypatch.setenv("RRTE_TILE_CULL", tc)
+        rts[tc] = Raytracer(scenes.SCENES[name](64, 36, mode="lambert_shadow")[3], device=0, jit=jit)
+    for w, h in ((131, 77), (200, 112)):
+        for k, (pos, tgt, fov) in enumerate(poses):
+            objs, lights, _, cfg = scenes.SCENES[name](w, h, mode="lambert_shadow")
+            if k == 5:
+                cfg.samples_per_pixel, cfg.jitter = 2, "random"
+            cam = scenes._camera(w, h, pos, tgt, fov)
+            out = {}
+            for tc, rt in rts.items():
+                rt.update_config(cfg)
+                _, lin = rt.render_f32(objs, lights, [], cam, linear=True)
+                out[tc] = (lin.view(np.uint32).copy(), int(rt.stats().shadow_rays))
+            assert np.array_equal(out["0"][0], out["1"][0]), (name, w, h, pos)
+            assert out["0"][1] == out["1"][1]
+
+
 def test_scene_cache_invalidates_on_change():
     objs, lights, cam, cfg = scenes.sdf_showcase(96, 54)
     rt = Raytracer(cfg, device=0, jit=abi.JIT_OFF)
