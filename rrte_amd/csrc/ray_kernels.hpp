@@ -1378,19 +1378,22 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
     return (b * kp.nranks + kp.rank) * kp.band_rows + w;
 }
 
-// Camera-ray tile culling mask of this workgroup's 16x16-pixel block (KParams::tile_rect): wave-
-// uniform, scalar ALU only.  The host enables it only when a block's 16 local rows are 16
+// Camera-ray tile culling mask of this workgroup's 16x16-pixel block (KParams::tile_rect): lane j
+// tests object j's rectangle and a ballot makes the mask wave-uniform (one load and a handful of
+// VALU ops per wave; a scalar loop over the objects cost ~8 SALU ops and a scalar load each).  Call
+// with all 64 lanes active.  The host enables it only when a block's 16 local rows are 16
 // consecutive image rows (no band mapping, or bands of a multiple of 16 rows).
 __device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp) {
     if (!kp.tile_cull) return ~0u;
     const uint32_t bx = blockIdx.x, by = image_row(kp, blockIdx.y * 16u) >> 4;
-    uint32_t m = kp.tile_n < 32u ? (~0u << kp.tile_n) : 0u;  // objects past the table: never culled
-#pragma unroll 1
-    for (uint32_t i = 0; i < kp.tile_n; ++i) {
-        const uint32_t t = kp.tile_rect[i];
-        if (bx >= (t & 255u) && bx <= ((t >> 8) & 255u) && by >= ((t >> 16) & 255u) && by <= (t >> 24)) m |= 1u << i;
+    const uint32_t j = threadIdx.x & 63u;
+    bool in = false;
+    if (j < kp.tile_n) {
+        const uint32_t t = kp.tile_rect[j];
+        in = bx >= (t & 255u) && bx <= ((t >> 8) & 255u) && by >= ((t >> 16) & 255u) && by <= (t >> 24);
     }
-    return __builtin_amdgcn_readfirstlane(m);
+    const uint32_t m = (uint32_t)__ballot(in);
+    return m | (kp.tile_n < 32u ? (~0u << kp.tile_n) : 0u);  // objects past the table: never culled
 }
 
 // One lane per pixel; wave = 8x8 tile, workgroup = 16x16 pixels.  Every lane
