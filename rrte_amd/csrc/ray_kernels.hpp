@@ -1378,14 +1378,18 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
     return (b * kp.nranks + kp.rank) * kp.band_rows + w;
 }
 
-// Camera-ray tile culling mask of this workgroup's 16x16-pixel block (KParams::tile_rect): lane j
-// tests object j's rectangle and a ballot makes the mask wave-uniform (one load and a handful of
-// VALU ops per wave; a scalar loop over the objects cost ~8 SALU ops and a scalar load each).  Call
-// with all 64 lanes active.  The host enables it only when a block's 16 local rows are 16
-// consecutive image rows (no band mapping, or bands of a multiple of 16 rows).
+// Camera-ray tile culling mask of this wave's 8x8 tile (kp.tile_cull = 3) or its workgroup's 16x16
+// block (4) (KParams::tile_rect): lane j tests object j's rectangle and a ballot makes the mask
+// wave-uniform (one load and a handful of VALU ops per wave; a scalar loop over the objects cost ~8
+// SALU ops and a scalar load each).  Call with all 64 lanes active.  The host enables it only when
+// a tile's local rows are consecutive image rows (no band mapping, or bands of a multiple of the
+// tile height).
 __device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp) {
-    if (!kp.tile_cull) return ~0u;
-    const uint32_t bx = blockIdx.x, by = image_row(kp, blockIdx.y * 16u) >> 4;
+    const uint32_t sh = kp.tile_cull;
+    if (!sh) return ~0u;
+    const uint32_t wave = sh == 3u ? (threadIdx.x >> 6) : 0u;
+    const uint32_t bx = (blockIdx.x * 16u + (wave & 1u) * 8u) >> sh;
+    const uint32_t by = image_row(kp, blockIdx.y * 16u + (wave >> 1) * 8u) >> sh;
     const uint32_t j = threadIdx.x & 63u;
     bool in = false;
     if (j < kp.tile_n) {

@@ -505,7 +505,8 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
 }
 
 // Camera-ray tile culling (KParams::tile_rect, ray_kernels.hpp camera_tile_mask), perspective frames:
-// for each of the first 32 objects, the 16x16-pixel blocks whose camera rays can reach its culling
+// for each of the first 32 objects, the 8x8-pixel tiles (16x16 for frames wider or taller than 2048)
+// whose camera rays can reach its culling
 // sphere (the conservative bound shadow culling uses: centre, radius).  In camera space a ray
 // direction (x, y, -1) that meets the sphere projects, in the xz plane, onto a line through the eye
 // that meets the sphere's disc there, so x lies between the tangents of that disc (likewise y in the
@@ -516,10 +517,18 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
 // (tests/test_gpu_parity.py test_camera_tile_culling_is_exact).
 void fill_tile_rects(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& k) {
     k.tile_cull = 0;
-    const uint32_t nbx = (p->width + 15) / 16, nby = (p->height + 15) / 16;
-    if (!c->env_tile_cull || s->camera.projection != RRTE_PERSPECTIVE || nbx > 256 || nby > 256 ||
-        (k.band_rows != 0 && k.band_rows % 16 != 0) || c->h_bounds.size() < s->num_prims)
+    // 8x8 tiles (one per wave) when their indices fit 8 bits and bands keep 8-row tiles whole,
+    // else 16x16 blocks (one per workgroup)
+    auto fits = [&](uint32_t sh) {
+        const uint32_t t = 1u << sh;
+        return (p->width + t - 1) / t <= 256 && (p->height + t - 1) / t <= 256 &&
+               (k.band_rows == 0 || k.band_rows % t == 0);
+    };
+    const uint32_t sh = fits(3) ? 3u : (fits(4) ? 4u : 0u);
+    if (!c->env_tile_cull || s->camera.projection != RRTE_PERSPECTIVE || sh == 0 ||
+        c->h_bounds.size() < s->num_prims)
         return;
+    const uint32_t nbx = (p->width + (1u << sh) - 1) >> sh, nby = (p->height + (1u << sh) - 1) >> sh;
     const rrte_camera& cam = s->camera;
     double q[4] = {cam.rotation[0], cam.rotation[1], cam.rotation[2], cam.rotation[3]};
     const double qn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
@@ -565,8 +574,8 @@ void fill_tile_rects(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_rende
                 if (px1 < 0.0 || py1 < 0.0 || px0 > W - 1.0 || py0 > H - 1.0) {
                     rect = 0xFFu | (0xFFu << 16);  // bx0 = 255 > bx1 = 0: no block (block indices <= 255)
                 } else {
-                    auto blk = [](double px, uint32_t nb) {
-                        const double b = std::floor(px / 16.0);
+                    auto blk = [sh](double px, uint32_t nb) {
+                        const double b = std::floor(px / (double)(1u << sh));
                         return (uint32_t)std::min<double>(std::max<double>(b, 0.0), (double)(nb - 1));
                     };
                     rect = blk(px0, nbx) | (blk(px1, nbx) << 8) | (blk(py0, nby) << 16) | (blk(py1, nby) << 24);
@@ -576,7 +585,7 @@ void fill_tile_rects(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_rende
         k.tile_rect[i] = rect;
     }
     k.tile_n = n;
-    k.tile_cull = 1;
+    k.tile_cull = sh;
 }
 
 uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank) {

@@ -218,8 +218,8 @@ def test_camera_motion_on_one_specialised_kernel(name):
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
 @pytest.mark.parametrize("name", ["sdf-showcase", "sdf-showcase-literal", "advanced-demo", "basic-demo"])
 def test_camera_tile_culling_is_exact(name, jit, monkeypatch):
-    """Camera-ray tile culling (KParams::tile_rect: a 16x16 block skips objects whose bounding sphere
-    projects outside it) never changes a bit: off and on give identical linear images and shadow-ray
+    """Camera-ray tile culling (KParams::tile_rect: an 8x8 tile, or a 16x16 block in frames wider
+    than 2048, skips objects whose bounding sphere projects outside it) never changes a bit: off and on give identical linear images and shadow-ray
     counts for poses with objects off screen, at the frame edge, close to the eye and behind it,
     a wide and a narrow field of view, odd frame sizes and random jitter."""
     poses = [((0.0, 8.0, 20.0), (0.0, 2.0, 0.0), 45.0), ((-11.0, 2.5, -3.0), (4.0, 2.0, -8.0), 80.0),
@@ -229,7 +229,7 @@ def test_camera_tile_culling_is_exact(name, jit, monkeypatch):
     for tc in ("0", "1"):  # the switch is read when a context is created
         monkeypatch.setenv("RRTE_TILE_CULL", tc)
         rts[tc] = Raytracer(scenes.SCENES[name](64, 36, mode="lambert_shadow")[3], device=0, jit=jit)
-    for w, h in ((131, 77), (200, 112)):
+    for w, h in ((131, 77), (200, 112), (2101, 40)):  # 8x8 tiles; 16x16 blocks past 2048 pixels
         for k, (pos, tgt, fov) in enumerate(poses):
             objs, lights, _, cfg = scenes.SCENES[name](w, h, mode="lambert_shadow")
             if k == 5:
