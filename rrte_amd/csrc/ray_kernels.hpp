@@ -282,7 +282,7 @@ __device__ __forceinline__ bool sdf_guard(const rrte_sdf_node& g, float a, f3 p,
         r = a;
         break;
     case RRTE_SDF_DIFFERENCE:
-        ok = ok && !(-L > a);
+        ok = ok && -L <= a;  // a NaN left operand fails the guard (smx(NaN, -b) is -b, not a)
         r = a;
         break;
     case RRTE_SDF_SMOOTH_UNION:
@@ -1409,8 +1409,15 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
                                                 uint32_t* __restrict__ out_rgba8, float4* __restrict__ out_f32,
                                                 unsigned long long* __restrict__ counters) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    // RRTE_DEBUG bit 4 (diagnostics, tools/wave_times.py): per-wave start / duration from the 100 MHz
+    // wall clock into the f32 buffer instead of colours
+    const bool stamps = (kp.debug & 16u) && out_f32;
+    // bit 5: only workgroup (debug >> 16) runs (its waves' durations alone on the GPU)
+    const uint32_t brow = blockIdx.y;
+    if ((kp.debug & 32u) && brow * gridDim.x + blockIdx.x != (kp.debug >> 16)) return;
+    const uint64_t t_wave0 = stamps ? wall_clock64() : 0ull;
     const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t lr = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const uint32_t lr = brow * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool live = x < kp.width && lr < kp.rows;
     const uint32_t xc = live ? x : 0u;
     const uint32_t y = image_row(kp, live ? lr : 0u);
@@ -1484,7 +1491,7 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
         const float ga = rclamp(acc.a);
         const size_t o = (size_t)lr * kp.width + x;  // packed local rows
         // the parity float buffer (or a gamma other than the reference's 2.2) needs powf itself
-        const bool exact_pow = out_f32 || ig != kInvGamma22;
+        const bool exact_pow = (out_f32 && !stamps) || ig != kInvGamma22;
         float gr = 0.0f, gg = 0.0f, gb = 0.0f;
         if (exact_pow) {
             gr = rclamp(powf(acc.r, ig));
@@ -1504,7 +1511,7 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
                 out_rgba8[o] = px;
             }
         }
-        if (out_f32) {
+        if (out_f32 && !stamps) {
             if (kp.flags & RRTE_FLAG_F32_LINEAR)
                 out_f32[o] = make_float4(acc.r, acc.g, acc.b, acc.a);
             else
@@ -1522,6 +1529,15 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
             const uint32_t shard = (blockIdx.x + blockIdx.y * gridDim.x + threadIdx.x / 64u * 61u) & (kCounterShards - 1u);
             atomicAdd(counters + shard * kCounterStride, (unsigned long long)v);
         }
+    }
+    if (stamps && lane == 0) {
+        const uint64_t t1 = wall_clock64();
+        const uint32_t wid = (brow * gridDim.x + blockIdx.x) * 4u + wave;
+        uint32_t* s = reinterpret_cast<uint32_t*>(out_f32) + 4u * wid;
+        s[0] = (uint32_t)t_wave0;
+        s[1] = (uint32_t)(t_wave0 >> 32);
+        s[2] = (uint32_t)(t1 - t_wave0);
+        s[3] = __smid();
     }
 }
 

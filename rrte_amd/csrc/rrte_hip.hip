@@ -665,6 +665,9 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
     } else {
         if (!(c->jit_mode == RRTE_JIT_ON || c->same_scene_renders >= 1)) return nullptr;
         if (c->jit_cache.size() >= 32) {
+            // frames launched from these modules may still run on caller streams (a mode / cull /
+            // sample-count change does not re-upload the scene, so upload_scene's sync has not run)
+            if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
             for (auto& kv : c->jit_cache) jit_release(kv.second);
             c->jit_cache.clear();
             last.valid = false;

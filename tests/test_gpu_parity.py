@@ -244,6 +244,92 @@ def test_camera_tile_culling_is_exact(name, jit, monkeypatch):
             assert out["0"][1] == out["1"][1]
 
 
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+@pytest.mark.parametrize("band", [8, 16])
+def test_camera_tile_culling_with_band_mapping(band, jit, monkeypatch):
+    """Tile culling on one rank's share of a multi-GPU frame (KParams::band_rows > 0: local rows map
+    to interleaved image rows through image_row): rank 1 of 3 emulated on one GPU
+    (RRTE_EMULATE_RANK, rrte_hip_render_async renders exactly that rank's packed bands).  Culling
+    on and off give identical linear rows, and they are the matching rows of the full frame."""
+    import torch
+    name, nranks, rank = "sdf-showcase", 3, 1
+    poses = [((0.0, 8.0, 20.0), (0.0, 2.0, 0.0), 45.0), ((-11.0, 2.5, -3.0), (4.0, 2.0, -8.0), 80.0),
+             ((3.0, 1.0, 3.0), (12.0, 2.0, 0.0), 100.0)]
+    full_rt = Raytracer(scenes.SCENES[name](64, 36, mode="lambert_shadow")[3], device=0, jit=jit)
+    ctxs = {}
+    monkeypatch.setenv("RRTE_EMULATE_RANK", f"{nranks}:{rank}")
+    for tc in ("0", "1"):  # both switches are read when a context is created
+        monkeypatch.setenv("RRTE_TILE_CULL", tc)
+        ctxs[tc] = Context(0, jit=jit)
+    monkeypatch.delenv("RRTE_EMULATE_RANK")
+    lib = abi.load()
+    for w, h in ((131, 77), (200, 112), (2101, 40)):  # 8x8 tiles; 16x16 blocks past 2048 pixels
+        rows = lib.rrte_hip_band_rows_for_rank(h, band, nranks, rank)
+        img_rows = [y for y in range(h) if (y // band) % nranks == rank]  # packed in image order
+        assert len(img_rows) == rows
+        for pos, tgt, fov in poses:
+            objs, lights, _, cfg = scenes.SCENES[name](w, h, mode="lambert_shadow")
+            cfg.band_rows = band
+            cam = scenes._camera(w, h, pos, tgt, fov)
+            full_rt.update_config(cfg)
+            _, full_lin = full_rt.render_f32(objs, lights, [], cam, linear=True)
+            full_lin = full_lin.view(np.uint32).reshape(h, w, 4)
+            sc = LoweredScene(objs, lights, cam)
+            prm = cfg.lower()
+            prm.flags |= abi.FLAG_F32_LINEAR
+            out = {}
+            for tc, ctx in ctxs.items():
+                f32 = torch.zeros(rows * w * 4, dtype=torch.float32, device="cuda")
+                ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), None, f32.data_ptr(), None))
+                ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+                out[tc] = f32.cpu().numpy().view(np.uint32).reshape(rows, w, 4)
+            assert np.array_equal(out["0"], out["1"]), (w, h, pos)
+            assert np.array_equal(out["1"], full_lin[img_rows]), (w, h, pos)
+    for ctx in ctxs.values():
+        ctx.close()
+
+
+def test_jit_cache_eviction_with_frames_in_flight():
+    """The scene-specialised kernel cache holds 32 modules; the 33rd (scene, mode, variant) evicts
+    them all.  A mode or sample-count change does not re-upload the scene (upload_scene's device sync
+    does not run), so the eviction itself must wait for frames still running from the old modules on
+    other streams.  Nine small scenes x up to four variants, every frame on one of four
+    streams without synchronising in between, the 33rd module requested on a same-scene variant
+    switch; every frame must equal the generic kernel's."""
+    import torch
+    W, H = 48, 32
+    variants = [("refcompat", 1), ("refcompat", 2), ("lambert_shadow", 1), ("lambert_shadow", 2)]
+    plan = []
+    for k in range(9):
+        n = 3 if k == 7 else 4  # 7*4 + 3 + 1 = 32 modules, then scene 9's second variant evicts
+        plan += [(k, v) for v in variants[:n]]
+    ctx = Context(0, jit=abi.JIT_ON)
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    frames = []
+    for i, (k, (mode, spp)) in enumerate(plan):
+        objs, lights, cam, cfg = scenes.basic_demo(W, H, mode=mode)
+        objs[1].radius = np.float32(0.6 + 0.05 * k)  # a distinct scene per k
+        cfg.samples_per_pixel, cfg.jitter = spp, ("random" if spp > 1 else "center")
+        sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+        for j in range(3):  # several frames of each variant in flight on different streams
+            buf = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            st = streams[(i + j) % 4]
+            ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), buf.data_ptr(), None,
+                                                    C.c_void_p(st.cuda_stream)))
+            frames.append((objs, lights, cam, cfg, buf))
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    assert ctx.stats().jit_active == 1
+    ctx.close()
+    rt = Raytracer(frames[0][3], device=0, jit=abi.JIT_OFF)
+    for objs, lights, cam, cfg, buf in frames[::3]:
+        rt.update_config(cfg)
+        ref = rt.render(objs, lights, [], cam)
+        assert np.array_equal(buf.cpu().numpy().view(np.uint8), ref)
+    for i in range(0, len(frames), 3):  # the other frames of each variant are identical to the first
+        a = frames[i][4].cpu()
+        assert all(torch.equal(a, frames[i + j][4].cpu()) for j in (1, 2))
+
+
 def test_scene_cache_invalidates_on_change():
     objs, lights, cam, cfg = scenes.sdf_showcase(96, 54)
     rt = Raytracer(cfg, device=0, jit=abi.JIT_OFF)

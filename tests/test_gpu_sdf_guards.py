@@ -21,12 +21,14 @@ def _render(args, jit):
 
 
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
-@pytest.mark.parametrize("case", ["deformation-stress", "random-csg-1", "random-csg-2", "sdf-showcase"])
+@pytest.mark.parametrize("case", ["deformation-stress", "random-csg-1", "random-csg-2", "sdf-showcase", "nan-left"])
 def test_csg_guards_are_exact(case, jit, monkeypatch):
     if case == "deformation-stress":
         args = scenes.deformation_stress(384, 216)
     elif case == "sdf-showcase":
         args = scenes.sdf_showcase(320, 180)
+    elif case == "nan-left":
+        args = se.nan_left_operand_scene(320, 180)
     else:
         args = se.random_csg_scene(320, 180, "lambert_shadow", seed=int(case[-1]))
     out = {}
