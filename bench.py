@@ -20,12 +20,11 @@ from pathlib import Path
 
 import numpy as np
 
-# Frames in flight need their streams on distinct hardware queues; HIP's default of 4 per
-# process is shared with torch's and the library's own streams (measured, tools/inflight_sweep.sh and
-# tools/inflight_q_sweep.sh: an N=8 rank's frame takes 40 us with 4 queues / 4 frames, 24 us with
-# 8 / 4, 17 us with 16 / 8, 14 us with 32 / 12; one GPU's whole frame is 95.5 us at all of the last three).
-# Must be set before HIP starts.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "32")
+# Frames in flight need their streams on distinct hardware queues.  HIP's default is 4 per process (the
+# GPU box exports GPU_MAX_HW_QUEUES=4), shared with torch's and the library's own streams; one rank of
+# an 8-GPU job then needs ~40 us for its share of a frame instead of ~24 us with 32 queues
+# (tools/r02_inflight.sh, 20 steps; the one-GPU frame is the same with 4 or 32).  Set before HIP starts.
+os.environ["GPU_MAX_HW_QUEUES"] = "32"
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -53,12 +52,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stock", action="store_true", help="skip the stock-config secondary measurement")
-    ap.add_argument("--inflight", type=int, default=12,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
-                         "so one frame's tail overlaps the next frame's start (1 = strictly one after another)")
-    ap.add_argument("--comm-stream", action="store_true",
-                    help="N > 1: run every frame's gather + de-interleave on the library's comm stream "
-                         "(RRTE_FLAG_GATHER_OVERLAP) instead of the frame's own stream")
+                         "so one frame's tail overlaps the next frame's start (1 = strictly one after another); "
+                         "default 4 on one GPU, 8 per rank for N > 1 (tools/r02_inflight.sh)")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
@@ -186,6 +183,7 @@ def main():
     if os.environ.get("RRTE_BENCH_DEVICE") is not None:
         local_rank = int(os.environ["RRTE_BENCH_DEVICE"])
     dist_on = world > 1
+    F = max(1, args.inflight if args.inflight is not None else (8 if world > 1 else 4))
     if dist_on:
         dist.init_process_group("gloo")  # control plane only; the frame gather is RCCL inside librrte_hip
     torch.cuda.set_device(local_rank)
@@ -201,13 +199,11 @@ def main():
         cfg.jitter = "random"
     scene = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
-    # N > 1: each frame's gather + de-interleave follow its render on the frame's own stream (frames in
-    # flight on other streams keep rendering meanwhile; the gathers stay in issue order through the
-    # library's event chain).  Measured on one GPU through a 1-rank communicator
-    # (tools/gather_overhead.py): +3.5 us per 1080p frame over the plain render, against +24 us when
-    # every gather is funnelled through the one comm stream (RRTE_FLAG_GATHER_OVERLAP, --comm-stream).
-    if world > 1 and args.comm_stream:
-        prm.flags |= abi.FLAG_GATHER_OVERLAP
+    # N > 1: frames render on their own streams and are gathered in batches of F (one ncclGather per F
+    # frames on the library's comm stream, rrte_hip_set_gather_batch): per-frame gathers chained
+    # across the F streams cost 50-90 us per rank-sized 1920x136 frame against 18 us for its render
+    # (tools/gather_variants.py, one GPU through a 1-rank communicator).  Every frame is still
+    # gathered to rank 0 and de-interleaved inside the timed region (flushed before its end).
     ctx = Context(local_rank, jit={"off": abi.JIT_OFF, "on": abi.JIT_ON, "auto": abi.JIT_AUTO}[args.jit])
     lib = ctx.lib
 
@@ -220,9 +216,9 @@ def main():
         dist.broadcast(uid, 0)
         idb = (C.c_uint8 * abi.UNIQUE_ID_BYTES)(*uid.tolist())
         ctx.check(lib.rrte_hip_comm_init(ctx.h, world, rank, idb))
+        ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, min(F, 16)))
 
     W, H = args.width, args.height
-    F = max(1, args.inflight)
     # dedicated (non-null) streams, one output buffer per frame in flight
     streams = [torch.cuda.Stream(dev) for _ in range(F)]
     fulls = [torch.empty(W * H, dtype=torch.int32, device=dev) for _ in range(F)]
@@ -260,6 +256,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    if dist_on:
+        ctx.check(lib.rrte_hip_flush(ctx.h))  # the last, partial gather batch
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if dist_on:
@@ -279,7 +277,10 @@ def main():
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
         primary, shadow = int(cnt[0].item()), int(cnt[1].item())
 
-    # single-frame latency (enqueue -> frame complete on the device), D2H of the frame separately
+    # single-frame latency (enqueue -> frame complete on the device), D2H of the frame separately;
+    # N > 1: each frame gathered on its own
+    if dist_on:
+        ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 1))
     lat = []
     for _ in range(5):
         if dist_on:
@@ -344,9 +345,7 @@ def main():
                 "workload": f"{args.scene} {W}x{H}, {args.mode}, spp={prm.samples_per_pixel}, max_depth={prm.max_depth}, "
                             + ("random jitter" if args.random else "pixel-centre jitter")
                             + (f", {args.band_rows}-row bands interleaved over {world} GPUs + RCCL gather to rank 0"
-                               + (" on the comm stream" if args.comm_stream else
-                                  " on each frame's stream, frames in flight")
-                               if world > 1 else ""),
+                               f" in batches of {min(F, 16)} frames" if world > 1 else ""),
                 "scene": args.scene, "width": W, "height": H, "mode": args.mode,
                 "primary_rays_per_frame": W * H * prm.samples_per_pixel,
                 "shadow_rays_per_frame": shadow // args.steps,

@@ -212,11 +212,9 @@ typedef enum rrte_jitter {
 } rrte_jitter;
 
 #define RRTE_FLAG_F32_LINEAR 1u  /* f32 output holds the averaged linear colour (pre-gamma, unclamped) */
-/* rrte_hip_render_gather_async only: pipeline frames.  The gather + de-interleave of
- * frame k run on the context's comm stream while frame k+1 renders on the caller's
- * stream (double-buffered slabs, event-ordered); the caller's stream is NOT made to
- * wait for the gather, so d_full_rgba8 is complete after rrte_hip_synchronize or a
- * device-wide synchronisation (SURVEY §8e "overlap frame k's gather with k+1's render"). */
+/* Accepted and ignored (ABI v2 compatibility).  It used to move each frame's gather onto a comm
+ * stream; frames now overlap on the caller's streams through the gather lanes of
+ * rrte_hip_comm_init (one communicator per lane), which measured faster. */
 #define RRTE_FLAG_GATHER_OVERLAP 2u
 
 typedef struct rrte_render_params {
@@ -348,11 +346,24 @@ rrte_status rrte_hip_comm_init(rrte_ctx* ctx, int nranks, int rank,
 rrte_status rrte_hip_render_gather(rrte_ctx* ctx, const rrte_scene_ir* scene,
                                    const rrte_render_params* params, int root,
                                    uint8_t* out_rgba8);
-/* Async device variant: d_full_rgba8 (root only, W*H*4 bytes) receives the frame;
- * all work is ordered on `stream` unless params->flags has RRTE_FLAG_GATHER_OVERLAP. */
+/* Async device variant: d_full_rgba8 (root only, W*H*4 bytes) receives the frame.  With gather batch 1
+ * (the default) all of the frame's work is ordered on `stream`; a frame on another stream than the
+ * previous frame's gather waits for that gather (collectives run in issue order on every rank).
+ * Every rank must issue the same frames in the same order. */
 rrte_status rrte_hip_render_gather_async(rrte_ctx* ctx, const rrte_scene_ir* scene,
                                          const rrte_render_params* params, int root,
                                          void* d_full_rgba8, void* stream);
+
+/* Batched gather (throughput mode, SURVEY §8e "fewer, larger collectives"): with frames > 1 each
+ * rrte_hip_render_gather_async renders this rank's bands on `stream` into the open batch, and every
+ * `frames` frames ONE ncclGather on the context's comm stream moves all of them to the root, which
+ * de-interleaves each into its d_full_rgba8.  A frame's d_full_rgba8 is then complete only after
+ * rrte_hip_flush + a synchronisation of the device, or rrte_hip_synchronize (which flushes).  A frame
+ * of another size, band height, root or slab format closes the open batch; so does a blocking
+ * rrte_hip_render_gather.  frames in [1, 16]; every rank must use the same setting.  Flushing with
+ * no open batch does nothing. */
+rrte_status rrte_hip_set_gather_batch(rrte_ctx* ctx, uint32_t frames);
+rrte_status rrte_hip_flush(rrte_ctx* ctx);
 
 /* Host-side helpers exported for the bindings (no device work). */
 /* Rows owned by `rank` under band interleave, in the order they are packed. */

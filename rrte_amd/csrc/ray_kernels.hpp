@@ -1573,4 +1573,33 @@ __global__ __launch_bounds__(256) void deinterleave_kernel(const uint8_t* __rest
     }
 }
 
+// Batched form (rrte_hip_set_gather_batch): the gathered buffer holds, per rank (rank_stride bytes
+// each), that rank's slices of `gridDim.z` frames back to back (frame_stride bytes each); frame z
+// goes to full[z].
+struct DeinterleaveTargets {
+    uint32_t* full[16];
+};
+template <bool RGB24>
+__global__ __launch_bounds__(256) void deinterleave_batch_kernel(const uint8_t* __restrict__ gathered,
+                                                                 DeinterleaveTargets t, uint32_t width,
+                                                                 uint32_t band_rows, uint32_t nranks,
+                                                                 size_t rank_stride, size_t frame_stride) {
+    const uint32_t y = blockIdx.y;
+    const uint32_t band = y / band_rows, w = y - band * band_rows;
+    const uint32_t rank = band % nranks, local_band = band / nranks;
+    const uint32_t lr = local_band * band_rows + w;
+    constexpr uint32_t bpp = RGB24 ? 3u : 4u;
+    const uint8_t* src = gathered + (size_t)rank * rank_stride + (size_t)blockIdx.z * frame_stride +
+                         (size_t)lr * width * bpp;
+    uint32_t* dst = t.full[blockIdx.z] + (size_t)y * width;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < width; x += gridDim.x * blockDim.x) {
+        if constexpr (RGB24) {
+            const uint8_t* q = src + 3u * x;
+            dst[x] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | 0xFF000000u;
+        } else {
+            dst[x] = reinterpret_cast<const uint32_t*>(src)[x];
+        }
+    }
+}
+
 }  // namespace rrte

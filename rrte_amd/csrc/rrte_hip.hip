@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -59,19 +60,38 @@ struct rrte_ctx {
     int nranks = 1, rank = 0;
     uint32_t* d_gather = nullptr; size_t cap_gather = 0;
     uint32_t* d_full = nullptr; size_t cap_full = 0;
-    // pipelined gather (RRTE_FLAG_GATHER_OVERLAP): consecutive frames alternate between two
-    // communicators (the second split from the first) on two comm streams, so the gathers of
-    // neighbouring frames overlap; slabs are a ring, everything event-ordered
-    static constexpr int kComms = 2;
-    int ncomms = 1;  // RRTE_GATHER_COMMS=2 enables the second communicator (opt-in: see comm_init)
-    ncclComm_t gcomm[kComms] = {};
-    hipStream_t gstream[kComms] = {};
-    static constexpr int kSlabs = 16;  // frames whose gather may be in flight at once
-    hipEvent_t ev_rend[kSlabs] = {}, ev_gath[kSlabs] = {};
+    static constexpr int kSlabs = 16;  // per-frame gathers (batch 1) that may be in flight at once
+    hipEvent_t ev_gath[kSlabs] = {};
+    hipStream_t slab_stream[kSlabs] = {};  // stream of the slab's last user (nullptr: never used)
     uint32_t* d_slab[kSlabs] = {};
     size_t cap_slab[kSlabs] = {};
+    // the last collective issued (either form): gathers must run in issue order on every rank
+    hipStream_t last_gather_stream = nullptr;
+    hipEvent_t last_gather_ev = nullptr;
+    // Batched gather (rrte_hip_set_gather_batch, B > 1): frames render on their own streams into the
+    // open batch's send slab; every B frames (or at rrte_hip_flush / synchronize) the comm stream
+    // waits for those renders, gathers all B frames to the root in ONE ncclGather and de-interleaves
+    // them.  Every collective is issued on the one comm stream, in program order.
+    static constexpr int kMaxBatch = 16, kBatchSlabs = 3;
+    static_assert(kMaxBatch == sizeof(rrte::DeinterleaveTargets::full) / sizeof(uint32_t*), "batch targets");
+    uint32_t gather_batch = 1;
+    hipStream_t comm_stream = nullptr;
+    struct Batch {
+        uint32_t n = 0, cap = 0;             // frames rendered into it / frames it was opened for
+        uint32_t width = 0, height = 0, band = 0;
+        int root = 0;
+        bool rgb24 = false;
+        size_t slice = 0;                    // bytes of one frame of one rank (256-B aligned)
+        uint32_t* full[kMaxBatch] = {};      // root: each frame's caller buffer
+        hipEvent_t ev_frame[kMaxBatch] = {}; // each frame's render done
+    } batch;
+    int bslot = 0;
+    hipEvent_t ev_batch[kBatchSlabs] = {};   // the slab's last batch gathered and de-interleaved
+    uint8_t* d_bsend[kBatchSlabs] = {};
+    size_t cap_bsend[kBatchSlabs] = {};
+    uint8_t* d_brecv[kBatchSlabs] = {};
+    size_t cap_brecv[kBatchSlabs] = {};
     uint64_t gather_frames = 0;
-    bool gather_timed = false;
     rrte_stats stats{};
     bool pending_kernel_timing = false;
     uint64_t pending_primary = 0;
@@ -96,9 +116,31 @@ struct rrte_ctx {
     std::unordered_map<std::string, JitKernel> jit_cache;  // failed compiles cached with fn == nullptr
     std::unordered_map<std::string, std::future<JitCode>> jit_pending;  // AUTO: background compiles
     std::string jit_log;
+    // RRTE_HOST_PROFILE=1 (diagnostics): host time per section of rrte_hip_render_gather_async,
+    // printed to stderr by rrte_hip_destroy
+    bool host_prof = false;
+    uint32_t env_diag_skip = 0;  // RRTE_DIAG_SKIP (1-rank timing diagnostics only): 1 no ncclGather, 2 no
+                                 // de-interleave, 4 no comm-stream waits -- results are wrong
+    double hp[10] = {};
+    uint64_t hp_frames = 0;
 };
 
 namespace {
+
+// Host-section timer for RRTE_HOST_PROFILE (no clock reads when it is off).
+struct HostSection {
+    rrte_ctx* c;
+    std::chrono::steady_clock::time_point t;
+    explicit HostSection(rrte_ctx* ctx) : c(ctx) {
+        if (c->host_prof) t = std::chrono::steady_clock::now();
+    }
+    void lap(int k) {
+        if (!c->host_prof) return;
+        const auto n = std::chrono::steady_clock::now();
+        c->hp[k] += std::chrono::duration<double, std::micro>(n - t).count();
+        t = n;
+    }
+};
 
 constexpr size_t kCounterBytes = sizeof(unsigned long long) * kCounterShards * kCounterStride;
 
@@ -712,7 +754,9 @@ rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params
         unsigned long long* ctr = c->d_counters;
         MeshView mv = c->mesh_view;
         void* args[] = {&k, &cl, &mv, &d_rgba, &d_f32, &ctr};
+        HostSection hs(c);
         HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, 1, 256, 1, 1, 0, st, args, nullptr));
+        hs.lap(8);
         return RRTE_OK;
     }
     if (p->mode == RRTE_MODE_REFCOMPAT)
@@ -827,6 +871,8 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     c->env_cull = env_cull_setting();
     if (const char* t = getenv("RRTE_TILE_CULL")) c->env_tile_cull = t[0] != '0';
     if (const char* g = getenv("RRTE_FORCE_GATHER")) c->env_force_gather = g[0] == '1';
+    if (const char* g = getenv("RRTE_HOST_PROFILE")) c->host_prof = g[0] == '1';
+    if (const char* g = getenv("RRTE_DIAG_SKIP")) c->env_diag_skip = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GATHER_RGB24")) c->env_gather_rgba = g[0] == '0';
     c->env_guard_leaves = env_guard_setting();
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
@@ -857,14 +903,18 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
 
 void rrte_hip_destroy(rrte_ctx* c) {
     if (!c) return;
+    if (c->host_prof && c->hp_frames) {
+        static const char* names[9] = {"validate", "upload_check", "slab_setup", "render_launch", "event_chain",
+                                       "ncclGather", "deinterleave", "event_record", "(of render_launch: the launch call)"};
+        fprintf(stderr, "rrte host profile (%llu gather frames, us/frame):", (unsigned long long)c->hp_frames);
+        for (int i = 0; i < 9; ++i) fprintf(stderr, " %s %.2f", names[i], c->hp[i] / (double)c->hp_frames);
+        fprintf(stderr, "\n");
+    }
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();  // frames may still run on caller streams
-    if (c->gcomm[1] && c->gcomm[1] != c->comm) ncclCommDestroy(c->gcomm[1]);
     if (c->comm) ncclCommDestroy(c->comm);
     c->jit_pending.clear();  // joins background compiles
     for (auto& kv : c->jit_cache) jit_release(kv.second);
-    for (hipStream_t gs : c->gstream)
-        if (gs) (void)hipStreamSynchronize(gs);
     void* bufs[] = {c->d_prims,      c->d_mats,      c->d_lights,     c->d_nodes,     c->d_bounds,
                     c->d_rgba,       c->d_f32,       c->d_counters,   c->d_gather,    c->d_full,
                     c->d_mesh_nodes, c->d_mesh_tris, c->d_mesh_norms, c->d_mesh_perm};
@@ -876,12 +926,17 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
-    for (int i = 0; i < rrte_ctx::kSlabs; ++i) {
-        if (c->ev_rend[i]) (void)hipEventDestroy(c->ev_rend[i]);
-        if (c->ev_gath[i]) (void)hipEventDestroy(c->ev_gath[i]);
+    for (hipEvent_t e : c->ev_gath)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_batch)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->batch.ev_frame)
+        if (e) (void)hipEventDestroy(e);
+    for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i) {
+        if (c->d_bsend[i]) (void)hipFree(c->d_bsend[i]);
+        if (c->d_brecv[i]) (void)hipFree(c->d_brecv[i]);
     }
-    for (hipStream_t gs : c->gstream)
-        if (gs) (void)hipStreamDestroy(gs);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -930,8 +985,12 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
     return RRTE_OK;
 }
 
+static rrte_status flush_batch(rrte_ctx* c);
+
 rrte_status rrte_hip_synchronize(rrte_ctx* c) {
     if (!c) return RRTE_INVALID_ARG;
+    rrte_status r = flush_batch(c);
+    if (r != RRTE_OK) return r;
     HIPCHK(c, hipDeviceSynchronize());
     return finish_frame(c);
 }
@@ -1033,23 +1092,15 @@ rrte_status rrte_hip_comm_unique_id(uint8_t out_id[RRTE_UNIQUE_ID_BYTES]) {
 rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t id_bytes[RRTE_UNIQUE_ID_BYTES]) {
     if (!c || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return fail(c, RRTE_INVALID_ARG, "bad comm args");
     HIPCHK(c, hipSetDevice(c->device));
-    if (c->comm) {
-        ncclCommDestroy(c->comm);
-        c->comm = nullptr;
-    }
-    if (c->gcomm[1] && c->gcomm[1] != c->comm) ncclCommDestroy(c->gcomm[1]);
-    c->gcomm[0] = c->gcomm[1] = nullptr;
+    HIPCHK(c, hipDeviceSynchronize());  // no gather of the old communicator may still run
+    if (c->comm) ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+    c->batch.n = 0;
+    c->last_gather_stream = nullptr;
+    c->last_gather_ev = nullptr;
     ncclUniqueId id;
     memcpy(&id, id_bytes, sizeof id);
     NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
-    // Optional second communicator over the same ranks (collective: every rank calls comm_init),
-    // so the pipelined gathers of neighbouring frames can overlap.  Opt-in: two communicators
-    // running concurrently are only deadlock-free while both their kernels can be resident at
-    // once, which this repository could not verify on more than one GPU.
-    const char* nc = getenv("RRTE_GATHER_COMMS");
-    c->ncomms = (nc && nc[0] == '2') ? 2 : 1;
-    if (c->ncomms == 2) NCCLCHK(c, ncclCommSplit(c->comm, 0, rank, &c->gcomm[1], nullptr));
-    c->gcomm[0] = c->comm;
     c->nranks = nranks;
     c->rank = rank;
     return RRTE_OK;
@@ -1072,16 +1123,62 @@ bool slab_rgb24(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_par
     return true;
 }
 
-rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
-                                         void* d_full, void* stream) {
-    if (!c) return RRTE_INVALID_ARG;
+// Issue the open batch (batched gather): the comm stream waits for its frames' renders, gathers all
+// of them to the root in one ncclGather (each rank sends its frames' slices back to back) and
+// de-interleaves every frame into its caller buffer.  Every rank holds the same open batch (same
+// frames in the same order), so the collective matches.
+static rrte_status flush_batch(rrte_ctx* c) {
+    rrte_ctx::Batch& b = c->batch;
+    if (b.n == 0) return RRTE_OK;
+    HostSection hs(c);
+    const int k = c->bslot;
+    if (!(c->env_diag_skip & 4u))
+        for (uint32_t j = 0; j < b.n; ++j) HIPCHK(c, hipStreamWaitEvent(c->comm_stream, b.ev_frame[j], 0));
+    if (c->last_gather_stream && c->last_gather_stream != c->comm_stream)
+        HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->last_gather_ev, 0));
+    const size_t count = (size_t)b.n * b.slice;  // bytes per rank
+    hs.lap(4);
+    if (!(c->env_diag_skip & 1u))
+        NCCLCHK(c, ncclGather(c->d_bsend[k], c->d_brecv[k], count, ncclUint8, b.root, c->comm, c->comm_stream));
+    hs.lap(5);
+    if (c->rank == b.root && !(c->env_diag_skip & 2u)) {
+        DeinterleaveTargets t{};
+        for (uint32_t j = 0; j < b.n; ++j) t.full[j] = b.full[j];
+        const dim3 dg((b.width + 255) / 256 < 8 ? (b.width + 255) / 256 : 8, b.height, b.n);
+        if (b.rgb24)
+            hipLaunchKernelGGL(deinterleave_batch_kernel<true>, dg, dim3(256), 0, c->comm_stream, c->d_brecv[k], t,
+                               b.width, b.band, (uint32_t)c->nranks, count, b.slice);
+        else
+            hipLaunchKernelGGL(deinterleave_batch_kernel<false>, dg, dim3(256), 0, c->comm_stream, c->d_brecv[k], t,
+                               b.width, b.band, (uint32_t)c->nranks, count, b.slice);
+        HIPCHK(c, hipGetLastError());
+    }
+    hs.lap(6);
+    HIPCHK(c, hipEventRecord(c->ev_batch[k], c->comm_stream));
+    c->last_gather_stream = c->comm_stream;
+    c->last_gather_ev = c->ev_batch[k];
+    c->bslot = (k + 1) % rrte_ctx::kBatchSlabs;
+    b.n = 0;
+    hs.lap(7);
+    return RRTE_OK;
+}
+
+// One multi-GPU frame on `st`: render this rank's bands into its slice of a gather slab, gather it to
+// the root and de-interleave there -- per frame (gather batch 1: everything on `st`, in place, the
+// frames' gathers chained across streams in issue order), or batched (the gather happens when the
+// open batch is full or flushed, on the comm stream).  `timing` (the blocking entry point): ev1 marks
+// the end of the render for rrte_stats.
+static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
+                                void* d_full, hipStream_t st, bool timing) {
+    HostSection hs(c);
     rrte_status r = validate(c, s, p);
     if (r != RRTE_OK) return r;
     if (root < 0 || root >= c->nranks) return fail(c, RRTE_INVALID_ARG, "root %d out of range", root);
     if (c->rank == root && !d_full) return fail(c, RRTE_INVALID_ARG, "root needs an output buffer");
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
     double up = 0.0;
+    hs.lap(0);
     if ((r = upload_scene(c, s, st, &up)) != RRTE_OK) return r;
+    hs.lap(1);
     const uint32_t band = p->band_rows ? p->band_rows : 16;
     rrte_render_params pp = *p;
     pp.band_rows = band;
@@ -1095,82 +1192,125 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, co
     if (c->nranks == 1 && !(c->env_force_gather && c->comm)) {
         r = launch(c, s, p, p->height, static_cast<uint32_t*>(d_full), nullptr, st);
         if (r == RRTE_OK) c->pending_primary = (uint64_t)p->width * p->height * p->samples_per_pixel;
+        if (timing) HIPCHK(c, hipEventRecord(c->ev1, st));
         return r;
     }
     if (!c->comm) return fail(c, RRTE_INVALID_ARG, "rrte_hip_comm_init has not been called");
-    const dim3 dg((p->width + 255) / 256 < 8 ? (p->width + 255) / 256 : 8, p->height);
-    if (!c->ev_rend[0]) {
-        for (int i = 0; i < rrte_ctx::kComms; ++i) HIPCHK(c, hipStreamCreateWithFlags(&c->gstream[i], hipStreamNonBlocking));
-        for (int i = 0; i < rrte_ctx::kSlabs; ++i) {
-            HIPCHK(c, hipEventCreateWithFlags(&c->ev_rend[i], hipEventDisableTiming));
-            HIPCHK(c, hipEventCreateWithFlags(&c->ev_gath[i], hipEventDisableTiming));
+    if (c->gather_batch > 1 && !timing) {
+        rrte_ctx::Batch& b = c->batch;
+        if (!c->comm_stream) {
+            HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+            for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i)
+                HIPCHK(c, hipEventCreateWithFlags(&c->ev_batch[i], hipEventDisableTiming));
+            for (int i = 0; i < rrte_ctx::kMaxBatch; ++i)
+                HIPCHK(c, hipEventCreateWithFlags(&b.ev_frame[i], hipEventDisableTiming));
         }
-    }
-    // slabs are a ring shared by every frame in flight, whatever stream it comes on: a frame
-    // waits until the previous user of its slab has been gathered
-    const int slot = (int)(c->gather_frames % rrte_ctx::kSlabs);
-    const size_t slab_words = slice * (size_t)c->nranks / 4u;
-    if (c->cap_slab[slot] < slab_words) {
-        // (re)size the whole ring at once: one device synchronisation (no slab may be freed under an
-        // in-flight gather) instead of one per slot spread over the first kSlabs frames
-        HIPCHK(c, hipDeviceSynchronize());
-        for (int i = 0; i < rrte_ctx::kSlabs; ++i)
-            if ((r = ensure(c, c->d_slab[i], c->cap_slab[i], slab_words)) != RRTE_OK) return r;
-    }
-    uint8_t* slab = reinterpret_cast<uint8_t*>(c->d_slab[slot]);
-    uint8_t* mine = slab + (size_t)c->rank * slice;  // in-place send slot
-    uint32_t* mine32 = reinterpret_cast<uint32_t*>(mine);
-    auto deinterleave = [&](hipStream_t ds) -> rrte_status {
-        if (rgb24)
-            hipLaunchKernelGGL(deinterleave_kernel<true>, dg, dim3(256), 0, ds, slab, static_cast<uint32_t*>(d_full),
-                               p->width, band, (uint32_t)c->nranks, slice);
-        else
-            hipLaunchKernelGGL(deinterleave_kernel<false>, dg, dim3(256), 0, ds, slab, static_cast<uint32_t*>(d_full),
-                               p->width, band, (uint32_t)c->nranks, slice);
-        HIPCHK(c, hipGetLastError());
-        return RRTE_OK;
-    };
-    HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[slot], 0));
-    if (!(p->flags & RRTE_FLAG_GATHER_OVERLAP)) {
-        // everything on `st`: render this rank's bands into its slot, gather in place, de-interleave.
-        // Gathers on one communicator must run in the same order on every rank: when frames come
-        // on several streams, each waits for the previous frame's gather.
-        if ((r = launch(c, s, &pp, rows, mine32, nullptr, st, kflags)) != RRTE_OK) return r;
-        HIPCHK(c, hipEventRecord(c->ev1, st));
-        if (c->gather_frames > 0)
-            HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[(c->gather_frames - 1) % rrte_ctx::kSlabs], 0));
-        NCCLCHK(c, ncclGather(mine, slab, slice, ncclUint8, root, c->comm, st));
-        if (c->rank == root && (r = deinterleave(st)) != RRTE_OK) return r;
-        HIPCHK(c, hipEventRecord(c->ev_gath[slot], st));
-        ++c->gather_frames;
+        // a frame of another size, band, root or slab format closes the open batch
+        if (b.n && (b.width != p->width || b.height != p->height || b.band != band || b.root != root ||
+                    b.rgb24 != rgb24 || b.slice != slice))
+            if ((r = flush_batch(c)) != RRTE_OK) return r;
+        const int k = c->bslot;
+        if (b.n == 0) {
+            b.cap = c->gather_batch;
+            b.width = p->width;
+            b.height = p->height;
+            b.band = band;
+            b.root = root;
+            b.rgb24 = rgb24;
+            b.slice = slice;
+            // every rank holds a receive slab too (the root's is the only one written)
+            const size_t send = (size_t)b.cap * slice, recv = send * (size_t)c->nranks;
+            if (c->cap_bsend[k] < send || c->cap_brecv[k] < recv) {
+                HIPCHK(c, hipDeviceSynchronize());  // no gather may still use the slab being resized
+                if ((r = ensure(c, c->d_bsend[k], c->cap_bsend[k], send)) != RRTE_OK) return r;
+                if ((r = ensure(c, c->d_brecv[k], c->cap_brecv[k], recv)) != RRTE_OK) return r;
+            }
+        }
+        // the slab is free once its previous batch has been gathered (usually long done)
+        HIPCHK(c, hipStreamWaitEvent(st, c->ev_batch[k], 0));
+        hs.lap(2);
+        uint8_t* mine = c->d_bsend[k] + (size_t)b.n * slice;
+        if ((r = launch(c, s, &pp, rows, reinterpret_cast<uint32_t*>(mine), nullptr, st, kflags)) != RRTE_OK) return r;
+        hs.lap(3);
+        HIPCHK(c, hipEventRecord(b.ev_frame[b.n], st));
+        b.full[b.n] = static_cast<uint32_t*>(d_full);
+        ++b.n;
+        if (b.n == b.cap && (r = flush_batch(c)) != RRTE_OK) return r;
     } else {
-        // Pipelined: frame k renders into slab k % kSlabs on `st` (frames may come on different
-        // streams and overlap); its gather + de-interleave run on comm stream k % ncomms with that
-        // communicator once the render's event fires -- one stream per communicator, so each
-        // communicator's gathers run in issue order on every rank.  The render of frame
-        // k + kSlabs (same slab) first waits for frame k's gather.  Waiting on a never-recorded
-        // event is a no-op.
-        const int lane = (int)(c->gather_frames % (uint64_t)c->ncomms);
-        ncclComm_t gc = c->gcomm[lane] ? c->gcomm[lane] : c->comm;
-        hipStream_t gs = c->gstream[lane];
-        if ((r = launch(c, s, &pp, rows, mine32, nullptr, st, kflags)) != RRTE_OK) return r;
-        HIPCHK(c, hipEventRecord(c->ev_rend[slot], st));
-        HIPCHK(c, hipStreamWaitEvent(gs, c->ev_rend[slot], 0));
-        NCCLCHK(c, ncclGather(mine, slab, slice, ncclUint8, root, gc, gs));
-        if (c->rank == root) {
-            // frames may finish out of order across the two comm streams: the de-interleave of frame k
-            // into d_full must not overtake frame k-1's (same output buffer when the caller reuses it)
-            if (c->gather_frames > 0)
-                HIPCHK(c, hipStreamWaitEvent(gs, c->ev_gath[(c->gather_frames - 1) % rrte_ctx::kSlabs], 0));
-            if ((r = deinterleave(gs)) != RRTE_OK) return r;
+        if ((r = flush_batch(c)) != RRTE_OK) return r;  // keep every rank's collectives in issue order
+        const dim3 dg((p->width + 255) / 256 < 8 ? (p->width + 255) / 256 : 8, p->height);
+        if (!c->ev_gath[0])
+            for (int i = 0; i < rrte_ctx::kSlabs; ++i)
+                HIPCHK(c, hipEventCreateWithFlags(&c->ev_gath[i], hipEventDisableTiming));
+        // slabs are a ring shared by every frame in flight: a frame on another stream than the slab's
+        // previous user waits until that frame has been gathered (same stream: stream order suffices)
+        const int slot = (int)(c->gather_frames % rrte_ctx::kSlabs);
+        const size_t slab_words = slice * (size_t)c->nranks / 4u;
+        if (c->cap_slab[slot] < slab_words) {
+            // (re)size the whole ring at once: one device synchronisation (no slab may be freed under an
+            // in-flight gather) instead of one per slot spread over the first kSlabs frames
+            HIPCHK(c, hipDeviceSynchronize());
+            for (int i = 0; i < rrte_ctx::kSlabs; ++i)
+                if ((r = ensure(c, c->d_slab[i], c->cap_slab[i], slab_words)) != RRTE_OK) return r;
         }
-        HIPCHK(c, hipEventRecord(c->ev_gath[slot], gs));
+        uint8_t* slab = reinterpret_cast<uint8_t*>(c->d_slab[slot]);
+        uint8_t* mine = slab + (size_t)c->rank * slice;  // in-place send slot
+        if (c->slab_stream[slot] && c->slab_stream[slot] != st)
+            HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[slot], 0));
+        hs.lap(2);
+        if ((r = launch(c, s, &pp, rows, reinterpret_cast<uint32_t*>(mine), nullptr, st, kflags)) != RRTE_OK) return r;
+        hs.lap(3);
+        if (timing) HIPCHK(c, hipEventRecord(c->ev1, st));
+        // gathers on one communicator must run in the same order on every rank: a frame on another
+        // stream than the previous gather waits for it
+        if (c->last_gather_stream && c->last_gather_stream != st)
+            HIPCHK(c, hipStreamWaitEvent(st, c->last_gather_ev, 0));
+        hs.lap(4);
+        NCCLCHK(c, ncclGather(mine, slab, slice, ncclUint8, root, c->comm, st));
+        hs.lap(5);
+        if (c->rank == root) {
+            if (rgb24)
+                hipLaunchKernelGGL(deinterleave_kernel<true>, dg, dim3(256), 0, st, slab, static_cast<uint32_t*>(d_full),
+                                   p->width, band, (uint32_t)c->nranks, slice);
+            else
+                hipLaunchKernelGGL(deinterleave_kernel<false>, dg, dim3(256), 0, st, slab, static_cast<uint32_t*>(d_full),
+                                   p->width, band, (uint32_t)c->nranks, slice);
+            HIPCHK(c, hipGetLastError());
+        }
+        hs.lap(6);
+        HIPCHK(c, hipEventRecord(c->ev_gath[slot], st));
+        c->slab_stream[slot] = st;
+        c->last_gather_stream = st;
+        c->last_gather_ev = c->ev_gath[slot];
+        hs.lap(7);
         ++c->gather_frames;
     }
+    ++c->hp_frames;
     c->pending_primary = (uint64_t)p->width * rows * p->samples_per_pixel;
     c->stats.upload_ms = up;
     c->stats.frames++;
     return RRTE_OK;
+}
+
+rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
+                                         void* d_full, void* stream) {
+    if (!c) return RRTE_INVALID_ARG;
+    return gather_frame(c, s, p, root, d_full, stream ? static_cast<hipStream_t>(stream) : c->stream, false);
+}
+
+rrte_status rrte_hip_set_gather_batch(rrte_ctx* c, uint32_t frames) {
+    if (!c) return RRTE_INVALID_ARG;
+    if (frames < 1 || frames > (uint32_t)rrte_ctx::kMaxBatch)
+        return fail(c, RRTE_INVALID_ARG, "gather batch %u outside [1, %d]", frames, rrte_ctx::kMaxBatch);
+    rrte_status r = flush_batch(c);
+    if (r != RRTE_OK) return r;
+    c->gather_batch = frames;
+    return RRTE_OK;
+}
+
+rrte_status rrte_hip_flush(rrte_ctx* c) {
+    if (!c) return RRTE_INVALID_ARG;
+    return flush_batch(c);
 }
 
 rrte_status rrte_hip_render_gather(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
@@ -1185,10 +1325,8 @@ rrte_status rrte_hip_render_gather(rrte_ctx* c, const rrte_scene_ir* s, const rr
         if ((r = ensure(c, c->d_full, c->cap_full, npix)) != RRTE_OK) return r;
         full = c->d_full;
     }
-    rrte_render_params pb = *p;
-    pb.flags &= ~RRTE_FLAG_GATHER_OVERLAP;  // one blocking frame: no pipelining
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    if ((r = rrte_hip_render_gather_async(c, s, &pb, root, full, c->stream)) != RRTE_OK) return r;
+    if ((r = gather_frame(c, s, p, root, full, c->stream, true)) != RRTE_OK) return r;
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     if (c->rank == root && out) HIPCHK(c, hipMemcpyAsync(out, full, npix * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -1,7 +1,9 @@
 """Multi-GPU frame path on one GPU: a 1-rank RCCL communicator with RRTE_FORCE_GATHER=1 drives
 rrte_hip_render_gather(_async) through the real band render -> ncclGather -> de-interleave
-sequence, in both the single-stream and the pipelined (RRTE_FLAG_GATHER_OVERLAP) form.  Every
-frame must equal the plain single-context render bit for bit.  (N > 1 needs more GPUs than the
+sequence, with frames in flight on three streams, gathered per frame or in batches of 3 or 8
+(rrte_hip_set_gather_batch: one ncclGather for a batch of frames on the comm stream; 7 frames leave
+a partial batch for the flush), and with the (now ignored) RRTE_FLAG_GATHER_OVERLAP.  Every frame
+must equal the plain single-context render bit for bit.  (N > 1 needs more GPUs than the
 test box has; the band partition itself is covered by tests/test_dist.py with gloo.)"""
 import ctypes as C
 
@@ -33,11 +35,11 @@ def _frames(n, w=320, h=200, alpha=None):
     return out
 
 
-@pytest.mark.parametrize("comms", ["1", "2"])
+@pytest.mark.parametrize("batch", [1, 3, 8])
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
-def test_gather_path_matches_plain_render(overlap, jit, comms, monkeypatch):
-    _check_gather(overlap, jit, comms, monkeypatch, None)
+def test_gather_path_matches_plain_render(overlap, jit, batch, monkeypatch):
+    _check_gather(overlap, jit, batch, monkeypatch, None)
 
 
 @pytest.mark.parametrize("alpha,rgb24", [(None, "0"), ("material", "1"), ("spp2", "1")])
@@ -45,14 +47,14 @@ def test_gather_slab_formats(alpha, rgb24, monkeypatch):
     """RGBA8 slabs when forced (RRTE_GATHER_RGB24=0) or when some alpha byte is not 255; every
     frame still equal to the plain render, alpha bytes included."""
     monkeypatch.setenv("RRTE_GATHER_RGB24", rgb24)
-    _check_gather(True, abi.JIT_ON, "1", monkeypatch, alpha)
+    _check_gather(True, abi.JIT_ON, 1, monkeypatch, alpha)
+    _check_gather(False, abi.JIT_ON, 4, monkeypatch, alpha)
 
 
-def _check_gather(overlap, jit, comms, monkeypatch, alpha):
+def _check_gather(overlap, jit, batch, monkeypatch, alpha):
     import torch
 
     monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
-    monkeypatch.setenv("RRTE_GATHER_COMMS", comms)
     frames = _frames(7, alpha=alpha)
     w, h = frames[0][1].width, frames[0][1].height
     ref = Context(0, jit=jit)
@@ -68,6 +70,7 @@ def _check_gather(overlap, jit, comms, monkeypatch, alpha):
     uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
     ctx.check(lib.rrte_hip_comm_unique_id(uid))
     ctx.check(lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
+    ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, batch))
     dev = torch.device("cuda", 0)
     streams = [torch.cuda.Stream(dev) for _ in range(3)]  # frames in flight, as bench.py runs them
     outs = [torch.empty(w * h, dtype=torch.int32, device=dev) for _ in frames]
@@ -100,4 +103,39 @@ def test_gather_requires_comm_and_root_buffer(monkeypatch):
     ctx.check(ctx.lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
     assert ctx.lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, None, None) == abi.RRTE_INVALID_ARG
     assert ctx.lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 1, None, None) == abi.RRTE_INVALID_ARG
+    ctx.close()
+
+
+def test_gather_batch_arguments_and_size_change(monkeypatch):
+    """Batch sizes outside [1, 16] are rejected; flushing with no open batch is a no-op; a frame of
+    another size closes the open batch (its frames are gathered first), and every frame of a stream
+    of alternating sizes still equals the plain render."""
+    import torch
+
+    monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    ctx = Context(0, jit=abi.JIT_ON)
+    lib = ctx.lib
+    uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+    ctx.check(lib.rrte_hip_comm_unique_id(uid))
+    ctx.check(lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
+    assert lib.rrte_hip_set_gather_batch(ctx.h, 0) == abi.RRTE_INVALID_ARG
+    assert lib.rrte_hip_set_gather_batch(ctx.h, 17) == abi.RRTE_INVALID_ARG
+    ctx.check(lib.rrte_hip_flush(ctx.h))
+    ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 4))
+    frames = [_frames(1, *((320, 200) if i % 3 else (160, 96)))[0] for i in range(8)]
+    ref = Context(0, jit=abi.JIT_OFF)
+    want = []
+    for sc, prm in frames:
+        buf = np.zeros(prm.width * prm.height * 4, dtype=np.uint8)
+        ref.check(ref.lib.rrte_hip_render(ref.h, sc.ref(), C.byref(prm), buf.ctypes.data_as(C.POINTER(C.c_uint8))))
+        want.append(buf)
+    ref.close()
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = [torch.empty(p.width * p.height, dtype=torch.int32, device="cuda") for _, p in frames]
+    for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
+        ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
+                                                    C.c_void_p(streams[i % 2].cuda_stream)))
+    ctx.check(lib.rrte_hip_synchronize(ctx.h))
+    for i, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint8), want[i]), f"frame {i}"
     ctx.close()

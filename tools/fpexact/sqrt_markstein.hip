@@ -1,0 +1,70 @@
+// Exhaustive check (all 2^32 f32 bit patterns) of residual-correction square roots against the
+// correctly rounded sqrt (the compiler's __builtin_sqrtf expansion): a faithful first
+// approximation s, its exact residual e = x - s*s (one fma), and one correction fma
+// r = s + e * h with h ~ 1/(2 sqrt x).  A NaN r (x = 0: e = 0, h = inf; x = inf: e = NaN) falls
+// back to s.  Prints one JSON line with the mismatch count and the first failing patterns.
+//   M1: s = v_sqrt_f32(x),     h = 0.5 * v_rsq_f32(x)
+//   M2: s = v_sqrt_f32(x),     h = 0.5 * v_rcp_f32(s)
+//   M3: s = x * v_rsq_f32(x),  h = 0.5 * v_rsq_f32(x)
+// build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -o sqrt_markstein sqrt_markstein.hip
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+
+constexpr int kCands = 3;
+
+__device__ __forceinline__ float fix(float r, float s) { return r != r ? s : r; }
+__device__ __forceinline__ float m1(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x), e = __builtin_fmaf(-s, s, x);
+    return fix(__builtin_fmaf(e, 0.5f * __builtin_amdgcn_rsqf(x), s), s);
+}
+__device__ __forceinline__ float m2(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x), e = __builtin_fmaf(-s, s, x);
+    return fix(__builtin_fmaf(e, 0.5f * __builtin_amdgcn_rcpf(s), s), s);
+}
+__device__ __forceinline__ float m3(float x) {
+    const float y = __builtin_amdgcn_rsqf(x), s = x * y, e = __builtin_fmaf(-s, s, x);
+    return fix(__builtin_fmaf(e, 0.5f * y, s), s);
+}
+
+struct Acc {
+    unsigned long long bad[kCands];
+    unsigned int nfirst[kCands];
+    unsigned int first[kCands][8];
+};
+
+__device__ __forceinline__ bool same(float a, float b) {
+    return (a != a && b != b) || __float_as_uint(a) == __float_as_uint(b);
+}
+
+__global__ __launch_bounds__(256) void sweep(uint32_t hi16, Acc* acc) {
+    const uint32_t xb = (hi16 << 16) | (blockIdx.x * 256u + threadIdx.x);
+    const float x = __uint_as_float(xb), want = __builtin_sqrtf(x);
+    const float got[kCands] = {m1(x), m2(x), m3(x)};
+    for (int k = 0; k < kCands; ++k) {
+        // inputs below 2^-96 (their residuals underflow) take the compiler's sequence in the kernels
+        const bool bad = !same(got[k], want) && !(__builtin_fabsf(x) < 0x1.0p-96f && x != 0.0f);
+        const unsigned long long m = __ballot(bad);
+        if (m && (threadIdx.x & 63u) == 0) atomicAdd(&acc->bad[k], (unsigned long long)__popcll(m));
+        if (bad && acc->nfirst[k] < 8u) {
+            const unsigned int n = atomicAdd(&acc->nfirst[k], 1u);
+            if (n < 8u) acc->first[k][n] = xb;
+        }
+    }
+}
+
+int main() {
+    Acc* d = nullptr;
+    if (hipMalloc(&d, sizeof(Acc)) != hipSuccess || hipMemset(d, 0, sizeof(Acc)) != hipSuccess) return 1;
+    for (uint32_t hi = 0; hi < 65536u; ++hi) hipLaunchKernelGGL(sweep, dim3(256), dim3(256), 0, 0, hi, d);
+    Acc h;
+    if (hipMemcpy(&h, d, sizeof(Acc), hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    printf("{");
+    for (int k = 0; k < kCands; ++k) {
+        printf("%s\"M%d\": {\"mismatches\": %llu, \"first\": [", k ? ", " : "", k + 1, h.bad[k]);
+        for (int i = 0; i < 8 && i < (int)h.nfirst[k]; ++i) printf("%s\"0x%08x\"", i ? ", " : "", h.first[k][i]);
+        printf("]}");
+    }
+    printf("}\n");
+    return hipFree(d) == hipSuccess ? 0 : 1;
+}
