@@ -94,24 +94,28 @@ constexpr uint32_t kFlagSlabRgb24 = 1u << 31;
 struct f3 { float x, y, z; };
 
 __device__ __forceinline__ f3 V(float x, float y, float z) { return f3{x, y, z}; }
-// Correctly rounded f32 sqrt (Rust f32::sqrt), 11 VALU ops instead of the compiler's 16.
-// v_sqrt_f32 is within 1 ulp; the neighbour whose residual x - s*(s -/+ ulp) changes sign
-// is taken (two fmas).  That is exact for every input except magnitudes in (0, 2^-96),
-// where the residuals underflow: those lanes (a divergent branch no real scene takes)
-// recompute with the compiler's scaled sequence.  Verified bit-identical to __builtin_sqrtf
-// over all 2^32 inputs on gfx950 (rrte_hip_fpcheck, tests/test_gpu_fpexact.py).
+// Correctly rounded f32 sqrt (Rust f32::sqrt), 6 VALU ops instead of the compiler's 16.
+// Verified bit-identical to __builtin_sqrtf over all 2^32 inputs on gfx950 (rrte_hip_fpcheck,
+// tests/test_gpu_fpexact.py).  (Round 1's form -- the neighbour of v_sqrt_f32 whose residual
+// x - s*(s -/+ ulp) changes sign, guarded below 2^-96 -- took 11.)
 // RRTE_ABLATE_FAST_SQRT swaps in the bare 1-ulp v_sqrt_f32 -- a timing experiment only
 // (breaks parity), never a build setting.
 #ifdef RRTE_ABLATE_FAST_SQRT
 __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_amdgcn_sqrtf(x); }
 #else
 __device__ __forceinline__ float sqrt_rn(float x) {
+    // one residual correction: s = v_sqrt_f32(x) (faithful), e = x - s*s exactly (one fma), and
+    // r = RN(s + e * h) with h = 0.5 * v_rsq_f32(x) ~ 1/(2 sqrt x): 5 VALU ops (two of them
+    // transcendental) against 9 for the two-sided neighbour test.  Correctly rounded for every x in
+    // [2^-96, FLT_MAX] (tools/fpexact/sqrt_markstein.hip: below it the residual underflows); every
+    // other x -- tiny, zero, denormal, negative, infinite, NaN -- takes the compiler's sequence in a
+    // divergent branch no real scene takes, chosen by one unsigned range test on the bits (positive
+    // floats order like their bit patterns; negatives and NaNs fall outside).
     const float s = __builtin_amdgcn_sqrtf(x);
-    const float lo = __uint_as_float(__float_as_uint(s) - 1u), hi = __uint_as_float(__float_as_uint(s) + 1u);
-    const float elo = __builtin_fmaf(-lo, s, x), ehi = __builtin_fmaf(-hi, s, x);
-    float r = (elo <= 0.0f) ? lo : s;
-    r = (ehi > 0.0f) ? hi : r;
-    if (__builtin_expect(__builtin_fabsf(x) < 0x1.0p-96f && x != 0.0f, 0)) r = __builtin_sqrtf(x);
+    const float e = __builtin_fmaf(-s, s, x);
+    float r = __builtin_fmaf(e, 0.5f * __builtin_amdgcn_rsqf(x), s);
+    constexpr uint32_t kLo = 0x0F800000u, kInf = 0x7F800000u;  // bits of 2^-96 and +inf
+    if (__builtin_expect(__float_as_uint(x) - kLo >= kInf - kLo, 0)) r = __builtin_sqrtf(x);
     return r;
 }
 #endif
