@@ -216,7 +216,7 @@ def main():
         dist.broadcast(uid, 0)
         idb = (C.c_uint8 * abi.UNIQUE_ID_BYTES)(*uid.tolist())
         ctx.check(lib.rrte_hip_comm_init(ctx.h, world, rank, idb))
-        ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, min(F, 16)))
+        ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, min(F, 16)))  # warm-up: the batched path
 
     W, H = args.width, args.height
     # dedicated (non-null) streams, one output buffer per frame in flight
@@ -230,8 +230,10 @@ def main():
     def step(i=0):
         j = i % F
         if dist_on:
+            # batched frames render on the library's own streams (multi-frame launches at the flush):
+            # one caller stream keeps the batch's dependency on its callers to one event
             ctx.check(lib.rrte_hip_render_gather_async(ctx.h, scene.ref(), C.byref(prm), 0,
-                                                       fulls[j].data_ptr() if rank == 0 else None, sptrs[j]))
+                                                       fulls[j].data_ptr() if rank == 0 else None, sptrs[0]))
         else:
             ctx.check(lib.rrte_hip_render_async(ctx.h, scene.ref(), C.byref(prm), fulls[j].data_ptr(), None, sptrs[j]))
 
@@ -240,6 +242,9 @@ def main():
     torch.cuda.synchronize(dev)
 
     # per-launch kernel duration (roofline): frames strictly one after another on one stream
+    # (N > 1: each frame rendered and gathered on its own)
+    if dist_on:
+        ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 1))
     n_seq = min(args.steps, 20)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_seq)]
     for i in range(n_seq):
@@ -251,6 +256,7 @@ def main():
     ctx.check(lib.rrte_hip_synchronize(ctx.h))  # folds warm-up and sequential-pass shadow counts away
 
     if dist_on:
+        ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, min(F, 16)))
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()

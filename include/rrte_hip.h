@@ -355,13 +355,15 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* ctx, const rrte_scene_ir* sce
                                          void* d_full_rgba8, void* stream);
 
 /* Batched gather (throughput mode, SURVEY §8e "fewer, larger collectives"): with frames > 1 each
- * rrte_hip_render_gather_async renders this rank's bands on `stream` into the open batch, and every
- * `frames` frames ONE ncclGather on the context's comm stream moves all of them to the root, which
- * de-interleaves each into its d_full_rgba8.  A frame's d_full_rgba8 is then complete only after
- * rrte_hip_flush + a synchronisation of the device, or rrte_hip_synchronize (which flushes).  A frame
- * of another size, band height, root or slab format closes the open batch; so does a blocking
- * rrte_hip_render_gather.  frames in [1, 16]; every rank must use the same setting.  Flushing with
- * no open batch does nothing. */
+ * rrte_hip_render_gather_async only records the frame (its camera is read, the scene uploaded if it
+ * changed) into the open batch; every `frames` frames the batch renders in multi-frame launches (up
+ * to 8 frames per launch) on the context's render streams, after the work already queued on the
+ * frames' streams, and ONE ncclGather on the context's comm stream moves all of them to the root,
+ * which de-interleaves each into its d_full_rgba8.  A frame's d_full_rgba8 is then complete only
+ * after rrte_hip_flush + a synchronisation of the device, or rrte_hip_synchronize (which flushes).
+ * A frame of another size, band height, root, slab format, mode or sampling setup closes the open
+ * batch, as do a scene change (any entry point) and a blocking rrte_hip_render_gather.  frames in
+ * [1, 16]; every rank must use the same setting.  Flushing with no open batch does nothing. */
 rrte_status rrte_hip_set_gather_batch(rrte_ctx* ctx, uint32_t frames);
 rrte_status rrte_hip_flush(rrte_ctx* ctx);
 

@@ -56,6 +56,27 @@ struct alignas(16) DLight {
 };
 static_assert(sizeof(DLight) == 96, "DLight layout");
 
+// The camera of one frame (camera.rs:24-31 after Camera::look_at; the per-frame part of the launch
+// constants) with its camera-ray tile-culling table.
+struct FrameCam {
+    uint32_t projection;
+    float cam_pos[3];
+    float cam_rot[4];
+    float half_h, aspect;
+    float ortho_l, ortho_r, ortho_b, ortho_t;
+    float cam_xf[12];
+    // Camera-ray tile culling (perspective frames, objects [0, tile_n), tile_n <= 32): object i's
+    // bounding sphere projects inside the tile rectangle tile_rect[i] = bx0 | bx1 << 8 | by0 << 16 |
+    // by1 << 24 (inclusive, conservative; tiles of 1 << tile_cull pixels: 3 = 8x8 per wave,
+    // 4 = 16x16 per workgroup); a tile outside it cannot hit object i with a camera ray.  0: off.
+    uint32_t tile_cull, tile_n;
+    uint32_t tile_rect[32];
+};
+
+// A launch renders up to kMaxLaunchFrames frames of one scene with the same parameters and their own
+// cameras (blockIdx.z = frame; batched multi-GPU frames, rrte_hip_set_gather_batch).
+constexpr uint32_t kMaxLaunchFrames = 8;
+
 // Per-launch constants, passed by value (kernel arguments land in SGPRs).
 struct KParams {
     uint32_t width, height;
@@ -68,20 +89,10 @@ struct KParams {
     uint32_t nranks, rank;
     float bg[4];
     float t_min, bias, inv_gamma, inv_spp;
-    // camera
-    uint32_t projection;
-    float cam_pos[3];
-    float cam_rot[4];
-    float half_h, aspect;
-    float ortho_l, ortho_r, ortho_b, ortho_t;
-    float cam_xf[12];
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
-    // Camera-ray tile culling (perspective frames, objects [0, tile_n), tile_n <= 32): object i's
-    // bounding sphere projects inside the tile rectangle tile_rect[i] = bx0 | bx1 << 8 | by0 << 16 |
-    // by1 << 24 (inclusive, conservative; tiles of 1 << tile_cull pixels: 3 = 8x8 per wave,
-    // 4 = 16x16 per workgroup); a tile outside it cannot hit object i with a camera ray.  0: off.
-    uint32_t tile_cull, tile_n;
-    uint32_t tile_rect[32];
+    uint32_t nframes;        // frames of this launch (gridDim.z), cam[0 .. nframes)
+    uint64_t frame_stride;   // bytes between consecutive frames' RGBA8 / slab outputs
+    FrameCam cam[kMaxLaunchFrames];
 };
 
 // Internal KParams::flags bit (never in the public rrte_render_params::flags): the launch writes

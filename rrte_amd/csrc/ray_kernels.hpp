@@ -1146,19 +1146,19 @@ __device__ __forceinline__ bool scatter(const DMaterial& m, const Ray& rin, cons
 struct Col { float r, g, b, a; };
 
 // Camera::generate_ray (camera.rs:98-133)
-__device__ __forceinline__ Ray generate_ray(const KParams& kp, float u, float v) {
+__device__ __forceinline__ Ray generate_ray(const FrameCam& cm, float u, float v) {
     float ndc_x = 2.0f * u - 1.0f;
     float ndc_y = 1.0f - 2.0f * v;
-    if (kp.projection == RRTE_PERSPECTIVE) {
-        float half_w = kp.aspect * kp.half_h;
-        f3 cd = vnorm(V(ndc_x * half_w, ndc_y * kp.half_h, -1.0f));
-        f3 wd = quat_rotate(kp.cam_rot, cd);
-        return ray_new(V(kp.cam_pos[0], kp.cam_pos[1], kp.cam_pos[2]), wd);
+    if (cm.projection == RRTE_PERSPECTIVE) {
+        float half_w = cm.aspect * cm.half_h;
+        f3 cd = vnorm(V(ndc_x * half_w, ndc_y * cm.half_h, -1.0f));
+        f3 wd = quat_rotate(cm.cam_rot, cd);
+        return ray_new(V(cm.cam_pos[0], cm.cam_pos[1], cm.cam_pos[2]), wd);
     }
-    float wx = kp.ortho_l + (kp.ortho_r - kp.ortho_l) * u;
-    float wy = kp.ortho_b + (kp.ortho_t - kp.ortho_b) * v;
-    f3 o = m_point(kp.cam_xf, V(wx, wy, 0.0f));
-    f3 wd = quat_rotate(kp.cam_rot, V(0.0f, 0.0f, -1.0f));
+    float wx = cm.ortho_l + (cm.ortho_r - cm.ortho_l) * u;
+    float wy = cm.ortho_b + (cm.ortho_t - cm.ortho_b) * v;
+    f3 o = m_point(cm.cam_xf, V(wx, wy, 0.0f));
+    f3 wd = quat_rotate(cm.cam_rot, V(0.0f, 0.0f, -1.0f));
     return ray_new(o, wd);
 }
 
@@ -1384,20 +1384,20 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
 // SALU ops and a scalar load each).  Call with all 64 lanes active.  The host enables it only when
 // a tile's local rows are consecutive image rows (no band mapping, or bands of a multiple of the
 // tile height).
-__device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp) {
-    const uint32_t sh = kp.tile_cull;
+__device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp, const FrameCam& cm) {
+    const uint32_t sh = cm.tile_cull;
     if (!sh) return ~0u;
     const uint32_t wave = sh == 3u ? (threadIdx.x >> 6) : 0u;
     const uint32_t bx = (blockIdx.x * 16u + (wave & 1u) * 8u) >> sh;
     const uint32_t by = image_row(kp, blockIdx.y * 16u + (wave >> 1) * 8u) >> sh;
     const uint32_t j = threadIdx.x & 63u;
     bool in = false;
-    if (j < kp.tile_n) {
-        const uint32_t t = kp.tile_rect[j];
+    if (j < cm.tile_n) {
+        const uint32_t t = cm.tile_rect[j];
         in = bx >= (t & 255u) && bx <= ((t >> 8) & 255u) && by >= ((t >> 16) & 255u) && by <= (t >> 24);
     }
     const uint32_t m = (uint32_t)__ballot(in);
-    return m | (kp.tile_n < 32u ? (~0u << kp.tile_n) : 0u);  // objects past the table: never culled
+    return m | (cm.tile_n < 32u ? (~0u << cm.tile_n) : 0u);  // objects past the table: never culled
 }
 
 // One lane per pixel; wave = 8x8 tile, workgroup = 16x16 pixels.  Every lane
@@ -1409,6 +1409,10 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
                                                 uint32_t* __restrict__ out_rgba8, float4* __restrict__ out_f32,
                                                 unsigned long long* __restrict__ counters) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    // frame blockIdx.z of the launch: its camera, its output (multi-frame launches have no f32 output)
+    const FrameCam& cm = kp.cam[blockIdx.z];
+    if (out_rgba8 && blockIdx.z)
+        out_rgba8 = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out_rgba8) + blockIdx.z * kp.frame_stride);
     // RRTE_DEBUG bit 4 (diagnostics, tools/wave_times.py): per-wave start / duration from the 100 MHz
     // wall clock into the f32 buffer instead of colours
     const bool stamps = (kp.debug & 16u) && out_f32;
@@ -1425,7 +1429,7 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     uint32_t nshadow = 0;
     Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
     const uint32_t nsamples = SINGLE ? 1u : kp.spp;
-    const uint32_t pmask = camera_tile_mask(kp);
+    const uint32_t pmask = camera_tile_mask(kp, cm);
     // camera ray of sample s (raytracer.rs:66-70): per-(pixel, sample) RNG stream, jitter, generate_ray
     auto camera_ray = [&](uint32_t s, uint32_t& st) {
         st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
@@ -1436,7 +1440,7 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
         }
         float u = ((float)xc + jx) / (float)kp.width;
         float v = ((float)y + jy) / (float)kp.height;
-        return generate_ray(kp, u, v);
+        return generate_ray(cm, u, v);
     };
     auto accumulate = [&](const Col& c) {
         acc.r = acc.r + c.r;

@@ -30,6 +30,17 @@
 
 using namespace rrte;
 
+// Everything one launch of the ray kernel needs, decided on the host from the scene and parameters.
+// A multi-frame launch (batched gather) is one plan whose KParams carry up to kMaxLaunchFrames
+// cameras: blockIdx.z picks the frame.
+struct LaunchPlan {
+    KParams k;
+    int mode;
+    bool cull, single;
+    uint32_t num_prims, num_lights, num_materials;
+    uint32_t gx, gy;
+};
+
 struct rrte_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -68,25 +79,33 @@ struct rrte_ctx {
     // the last collective issued (either form): gathers must run in issue order on every rank
     hipStream_t last_gather_stream = nullptr;
     hipEvent_t last_gather_ev = nullptr;
-    // Batched gather (rrte_hip_set_gather_batch, B > 1): frames render on their own streams into the
-    // open batch's send slab; every B frames (or at rrte_hip_flush / synchronize) the comm stream
-    // waits for those renders, gathers all B frames to the root in ONE ncclGather and de-interleaves
-    // them.  Every collective is issued on the one comm stream, in program order.
+    // Batched gather (rrte_hip_set_gather_batch, B > 1): a frame call only plans its render (camera,
+    // tile rectangles); every B frames (or at rrte_hip_flush / synchronize / a scene or parameter
+    // change) the batch renders in multi-frame launches (blockIdx.z = frame, up to kMaxLaunchFrames
+    // per launch) on the slab's render stream into the send slab, and the comm stream gathers all B
+    // frames to the root in ONE ncclGather and de-interleaves them.  Every collective is issued on
+    // the one comm stream, in program order; slab k's render stream overlaps slab k-1's gather.
     static constexpr int kMaxBatch = 16, kBatchSlabs = 3;
     static_assert(kMaxBatch == sizeof(rrte::DeinterleaveTargets::full) / sizeof(uint32_t*), "batch targets");
     uint32_t gather_batch = 1;
     hipStream_t comm_stream = nullptr;
+    hipStream_t render_stream[kBatchSlabs] = {};
     struct Batch {
-        uint32_t n = 0, cap = 0;             // frames rendered into it / frames it was opened for
+        uint32_t n = 0, cap = 0;             // frames planned into it / frames it was opened for
         uint32_t width = 0, height = 0, band = 0;
         int root = 0;
         bool rgb24 = false;
         size_t slice = 0;                    // bytes of one frame of one rank (256-B aligned)
+        LaunchPlan plan;                     // frame 0's plan; frame j's camera in cam[j % kMaxLaunchFrames]
+        FrameCam cam[kMaxBatch];
         uint32_t* full[kMaxBatch] = {};      // root: each frame's caller buffer
-        hipEvent_t ev_frame[kMaxBatch] = {}; // each frame's render done
+        uint32_t nsrc = 0;                   // distinct caller streams of the batch's frames
+        hipStream_t src[kMaxBatch] = {};
+        hipEvent_t ev_src[kMaxBatch] = {};   // recorded on src[i] at the flush
     } batch;
     int bslot = 0;
     hipEvent_t ev_batch[kBatchSlabs] = {};   // the slab's last batch gathered and de-interleaved
+    hipEvent_t ev_render[kBatchSlabs] = {};  // the slab's last batch rendered
     uint8_t* d_bsend[kBatchSlabs] = {};
     size_t cap_bsend[kBatchSlabs] = {};
     uint8_t* d_brecv[kBatchSlabs] = {};
@@ -124,6 +143,8 @@ struct rrte_ctx {
     double hp[10] = {};
     uint64_t hp_frames = 0;
 };
+
+static rrte_status flush_batch(rrte_ctx* c);
 
 namespace {
 
@@ -418,22 +439,52 @@ struct MeshKey {
     uint64_t nv, ni, version;
 };
 
-rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
-    const size_t bp = sizeof(rrte_prim) * s->num_prims, bm = sizeof(rrte_material) * s->num_materials,
-                 bl = sizeof(rrte_light) * s->num_lights, bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
-    const MeshKey mk{s->mesh_vertices, s->mesh_indices, s->num_mesh_vertices, s->num_mesh_indices, s->mesh_version};
+// The key parts of a scene IR (compared byte for byte against the cached scene's key).
+struct SceneKeyParts {
+    const void* parts[7];
+    size_t lens[7];
+    size_t total;
+    MeshKey mk;
+};
+void scene_key_parts(const rrte_scene_ir* s, SceneKeyParts& kp) {
+    kp.mk = MeshKey{s->mesh_vertices, s->mesh_indices, s->num_mesh_vertices, s->num_mesh_indices, s->mesh_version};
     const size_t bmv = s->mesh_version ? 0 : sizeof(rrte_mesh_vertex) * s->num_mesh_vertices;
     const size_t bmi = s->mesh_version ? 0 : sizeof(uint32_t) * s->num_mesh_indices;
-    const size_t key_len = bp + bm + bl + bn + sizeof(MeshKey) + bmv + bmi;
-    const void* parts[] = {s->prims, s->materials, s->lights, s->sdf_nodes, &mk, s->mesh_vertices, s->mesh_indices};
-    const size_t lens[] = {bp, bm, bl, bn, sizeof(MeshKey), bmv, bmi};
-    bool same = c->scene_key.size() == key_len;
-    if (same) {
-        const unsigned char* k = c->scene_key.data();
-        for (int i = 0; i < 7 && same; ++i) {
-            same = lens[i] == 0 || !memcmp(k, parts[i], lens[i]);
-            k += lens[i];
-        }
+    const void* parts[7] = {s->prims, s->materials, s->lights, s->sdf_nodes, &kp.mk, s->mesh_vertices, s->mesh_indices};
+    const size_t lens[7] = {sizeof(rrte_prim) * s->num_prims, sizeof(rrte_material) * s->num_materials,
+                            sizeof(rrte_light) * s->num_lights, sizeof(rrte_sdf_node) * s->num_sdf_nodes,
+                            sizeof(MeshKey), bmv, bmi};
+    kp.total = 0;
+    for (int i = 0; i < 7; ++i) {
+        kp.parts[i] = parts[i];
+        kp.lens[i] = lens[i];
+        kp.total += lens[i];
+    }
+}
+
+// True if `s` is the scene cached on the device (no upload needed).
+bool scene_same(const rrte_ctx* c, const rrte_scene_ir* s) {
+    SceneKeyParts kp;
+    scene_key_parts(s, kp);
+    if (c->scene_key.size() != kp.total) return false;
+    const unsigned char* k = c->scene_key.data();
+    for (int i = 0; i < 7; ++i) {
+        if (kp.lens[i] && memcmp(k, kp.parts[i], kp.lens[i])) return false;
+        k += kp.lens[i];
+    }
+    return true;
+}
+
+rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
+    const size_t bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
+    SceneKeyParts kparts;
+    scene_key_parts(s, kparts);
+    const size_t key_len = kparts.total;
+    const bool same = scene_same(c, s);
+    if (!same && c->batch.n) {
+        // the open batch renders the cached scene at its flush: render it before the scene changes
+        rrte_status r = flush_batch(c);
+        if (r != RRTE_OK) return r;
     }
     *upload_ms = 0.0;
     if (same) {
@@ -502,8 +553,8 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     c->scene_key.resize(key_len);
     unsigned char* k = c->scene_key.data();
     for (int i = 0; i < 7; ++i) {
-        if (lens[i]) memcpy(k, parts[i], lens[i]);
-        k += lens[i];
+        if (kparts.lens[i]) memcpy(k, kparts.parts[i], kparts.lens[i]);
+        k += kparts.lens[i];
     }
     return RRTE_OK;
 }
@@ -530,18 +581,21 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     k.bias = p->shadow_bias;
     k.inv_gamma = 1.0f / p->gamma;                        // raytracer.rs:79 -> color.rs:60
     k.inv_spp = 1.0f / (float)p->samples_per_pixel;       // raytracer.rs:76
+    k.nframes = 1;
+    k.frame_stride = 0;
     const rrte_camera& cam = s->camera;
-    k.projection = cam.projection;
-    memcpy(k.cam_pos, cam.position, sizeof k.cam_pos);
-    memcpy(k.cam_rot, cam.rotation, sizeof k.cam_rot);
-    k.half_h = tanf(cam.fov * 0.5f);                      // camera.rs:104
-    k.aspect = cam.aspect_ratio;
-    k.ortho_l = cam.left; k.ortho_r = cam.right; k.ortho_b = cam.bottom; k.ortho_t = cam.top;
+    FrameCam& fc = k.cam[0];
+    fc.projection = cam.projection;
+    memcpy(fc.cam_pos, cam.position, sizeof fc.cam_pos);
+    memcpy(fc.cam_rot, cam.rotation, sizeof fc.cam_rot);
+    fc.half_h = tanf(cam.fov * 0.5f);                     // camera.rs:104
+    fc.aspect = cam.aspect_ratio;
+    fc.ortho_l = cam.left; fc.ortho_r = cam.right; fc.ortho_b = cam.bottom; fc.ortho_t = cam.top;
     float trs[10] = {cam.position[0], cam.position[1], cam.position[2], cam.rotation[0], cam.rotation[1],
                      cam.rotation[2], cam.rotation[3], cam.scale[0], cam.scale[1], cam.scale[2]};
     float m[16];
     mat4_srt(trs, m);
-    to_affine12(m, k.cam_xf);
+    to_affine12(m, fc.cam_xf);
     k.debug = c->env_debug;  // RRTE_DEBUG ablation bits (profiling only)
     return k;
 }
@@ -557,14 +611,16 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
 // (inside the pixel).  A sphere that contains the eye or reaches the plane z = 0 keeps the whole
 // frame.  Bit-identical results by construction: a skipped test is one every lane would miss
 // (tests/test_gpu_parity.py test_camera_tile_culling_is_exact).
-void fill_tile_rects(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& k) {
+void fill_tile_rects(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& kk) {
+    FrameCam& k = kk.cam[0];
+    const uint32_t band_rows = kk.band_rows;
     k.tile_cull = 0;
     // 8x8 tiles (one per wave) when their indices fit 8 bits and bands keep 8-row tiles whole,
     // else 16x16 blocks (one per workgroup)
     auto fits = [&](uint32_t sh) {
         const uint32_t t = 1u << sh;
         return (p->width + t - 1) / t <= 256 && (p->height + t - 1) / t <= 256 &&
-               (k.band_rows == 0 || k.band_rows % t == 0);
+               (band_rows == 0 || band_rows % t == 0);
     };
     const uint32_t sh = fits(3) ? 3u : (fits(4) ? 4u : 0u);
     if (!c->env_tile_cull || s->camera.projection != RRTE_PERSPECTIVE || sh == 0 ||
@@ -734,39 +790,59 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
     return remember(slot.fn ? &slot : nullptr);
 }
 
-rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
-                   uint32_t* d_rgba, float4* d_f32, hipStream_t st, uint32_t internal_flags = 0u) {
-    KParams k = make_params(c, s, p, rows);
-    k.flags |= internal_flags;
-    SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, s->num_prims, s->num_lights, s->num_materials,
-                 c->mesh_view};
-    const bool cull = cull_policy(s, p->mode, c->env_cull);
-    Cull cl{cull ? c->d_bounds : nullptr, s->num_prims};
-    dim3 grid((p->width + 15) / 16, (rows + 15) / 16), block(256);
-    if (rows == 0) return RRTE_OK;
+LaunchPlan plan_launch(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
+                       uint32_t internal_flags) {
+    LaunchPlan L;
+    L.k = make_params(c, s, p, rows);
+    L.k.flags |= internal_flags;
+    L.mode = (int)p->mode;
+    L.cull = cull_policy(s, p->mode, c->env_cull);
     // single-sample, single-bounce frames get the straight-line specialisation (SINGLE); others the
     // specialisation with runtime sample / bounce loops
-    const bool single = p->samples_per_pixel == 1 && (p->mode == RRTE_MODE_LAMBERT_SHADOW || p->max_depth <= 1);
-    fill_tile_rects(c, s, p, k);
-    JitKernel* jk = jit_kernel_for(c, (int)p->mode, cull, single);
+    L.single = p->samples_per_pixel == 1 && (p->mode == RRTE_MODE_LAMBERT_SHADOW || p->max_depth <= 1);
+    L.num_prims = s->num_prims;
+    L.num_lights = s->num_lights;
+    L.num_materials = s->num_materials;
+    L.gx = (p->width + 15) / 16;
+    L.gy = (rows + 15) / 16;
+    fill_tile_rects(c, s, p, L.k);
+    return L;
+}
+
+// Launch plan `L` (L.k.nframes frames) on `st`; the cached scene is the plan's.
+rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
+    if (L.gy == 0) return RRTE_OK;
+    Cull cl{L.cull ? c->d_bounds : nullptr, L.num_prims};
+    const dim3 grid(L.gx, L.gy, L.k.nframes), block(256);
+    JitKernel* jk = jit_kernel_for(c, L.mode, L.cull, L.single);
     c->stats.jit_active = jk ? 1u : 0u;
     if (jk) {
         unsigned long long* ctr = c->d_counters;
         MeshView mv = c->mesh_view;
-        void* args[] = {&k, &cl, &mv, &d_rgba, &d_f32, &ctr};
+        void* args[] = {&L.k, &cl, &mv, &d_rgba, &d_f32, &ctr};
         HostSection hs(c);
-        HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, 1, 256, 1, 1, 0, st, args, nullptr));
+        HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, 256, 1, 1, 0, st, args, nullptr));
         hs.lap(8);
         return RRTE_OK;
     }
-    if (p->mode == RRTE_MODE_REFCOMPAT)
+    SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
+                 c->mesh_view};
+    const KParams& k = L.k;
+    if (L.mode == RRTE_MODE_REFCOMPAT)
         hipLaunchKernelGGL((ray_kernel<RRTE_MODE_REFCOMPAT, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
-    else if (cull)
+    else if (L.cull)
         hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, true>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     else
         hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     HIPCHK(c, hipGetLastError());
     return RRTE_OK;
+}
+
+rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
+                   uint32_t* d_rgba, float4* d_f32, hipStream_t st, uint32_t internal_flags = 0u) {
+    if (rows == 0) return RRTE_OK;
+    LaunchPlan L = plan_launch(c, s, p, rows, internal_flags);
+    return issue_launch(c, L, d_rgba, d_f32, st);
 }
 
 // Read back the device counters and close the frame's statistics.
@@ -930,11 +1006,14 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_batch)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->batch.ev_frame)
+    for (hipEvent_t e : c->ev_render)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->batch.ev_src)
         if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i) {
         if (c->d_bsend[i]) (void)hipFree(c->d_bsend[i]);
         if (c->d_brecv[i]) (void)hipFree(c->d_brecv[i]);
+        if (c->render_stream[i]) (void)hipStreamDestroy(c->render_stream[i]);
     }
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -984,8 +1063,6 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
     c->stats.frames++;
     return RRTE_OK;
 }
-
-static rrte_status flush_batch(rrte_ctx* c);
 
 rrte_status rrte_hip_synchronize(rrte_ctx* c) {
     if (!c) return RRTE_INVALID_ARG;
@@ -1132,11 +1209,32 @@ static rrte_status flush_batch(rrte_ctx* c) {
     if (b.n == 0) return RRTE_OK;
     HostSection hs(c);
     const int k = c->bslot;
+    const size_t count = (size_t)b.n * b.slice;  // bytes per rank
+    hipStream_t rs = c->render_stream[k];
+    // the renders follow the frames' caller streams (scene uploads, the callers' own prior work) and
+    // the slab's previous batch (its gather reads the send slab)
     if (!(c->env_diag_skip & 4u))
-        for (uint32_t j = 0; j < b.n; ++j) HIPCHK(c, hipStreamWaitEvent(c->comm_stream, b.ev_frame[j], 0));
+        for (uint32_t i = 0; i < b.nsrc; ++i) {
+            HIPCHK(c, hipEventRecord(b.ev_src[i], b.src[i]));
+            HIPCHK(c, hipStreamWaitEvent(rs, b.ev_src[i], 0));
+        }
+    HIPCHK(c, hipStreamWaitEvent(rs, c->ev_batch[k], 0));
+    hs.lap(2);
+    for (uint32_t j0 = 0; j0 < b.n; j0 += kMaxLaunchFrames) {
+        const uint32_t nf = std::min<uint32_t>(b.n - j0, kMaxLaunchFrames);
+        LaunchPlan& L = b.plan;
+        memcpy(L.k.cam, b.cam + j0, nf * sizeof(FrameCam));
+        L.k.nframes = nf;
+        L.k.frame_stride = b.slice;
+        uint8_t* dst = c->d_bsend[k] + (size_t)j0 * b.slice;
+        rrte_status r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, rs);
+        if (r != RRTE_OK) return r;
+    }
+    HIPCHK(c, hipEventRecord(c->ev_render[k], rs));
+    hs.lap(3);
+    HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
     if (c->last_gather_stream && c->last_gather_stream != c->comm_stream)
         HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->last_gather_ev, 0));
-    const size_t count = (size_t)b.n * b.slice;  // bytes per rank
     hs.lap(4);
     if (!(c->env_diag_skip & 1u))
         NCCLCHK(c, ncclGather(c->d_bsend[k], c->d_brecv[k], count, ncclUint8, b.root, c->comm, c->comm_stream));
@@ -1159,6 +1257,7 @@ static rrte_status flush_batch(rrte_ctx* c) {
     c->last_gather_ev = c->ev_batch[k];
     c->bslot = (k + 1) % rrte_ctx::kBatchSlabs;
     b.n = 0;
+    b.nsrc = 0;
     hs.lap(7);
     return RRTE_OK;
 }
@@ -1200,14 +1299,20 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         rrte_ctx::Batch& b = c->batch;
         if (!c->comm_stream) {
             HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-            for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i)
+            for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i) {
+                HIPCHK(c, hipStreamCreateWithFlags(&c->render_stream[i], hipStreamNonBlocking));
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_batch[i], hipEventDisableTiming));
+                HIPCHK(c, hipEventCreateWithFlags(&c->ev_render[i], hipEventDisableTiming));
+            }
             for (int i = 0; i < rrte_ctx::kMaxBatch; ++i)
-                HIPCHK(c, hipEventCreateWithFlags(&b.ev_frame[i], hipEventDisableTiming));
+                HIPCHK(c, hipEventCreateWithFlags(&b.ev_src[i], hipEventDisableTiming));
         }
-        // a frame of another size, band, root or slab format closes the open batch
+        LaunchPlan L = plan_launch(c, s, &pp, rows, kflags);
+        // a frame of another size, band, root, slab format or render setup closes the open batch
+        // (the cameras and tile rectangles are per frame; everything before KParams::nframes is not)
         if (b.n && (b.width != p->width || b.height != p->height || b.band != band || b.root != root ||
-                    b.rgb24 != rgb24 || b.slice != slice))
+                    b.rgb24 != rgb24 || b.slice != slice || b.plan.mode != L.mode || b.plan.cull != L.cull ||
+                    b.plan.single != L.single || memcmp(&b.plan.k, &L.k, offsetof(KParams, nframes))))
             if ((r = flush_batch(c)) != RRTE_OK) return r;
         const int k = c->bslot;
         if (b.n == 0) {
@@ -1218,23 +1323,23 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             b.root = root;
             b.rgb24 = rgb24;
             b.slice = slice;
+            b.plan = L;
             // every rank holds a receive slab too (the root's is the only one written)
             const size_t send = (size_t)b.cap * slice, recv = send * (size_t)c->nranks;
             if (c->cap_bsend[k] < send || c->cap_brecv[k] < recv) {
-                HIPCHK(c, hipDeviceSynchronize());  // no gather may still use the slab being resized
+                HIPCHK(c, hipDeviceSynchronize());  // no render or gather may still use the slab being resized
                 if ((r = ensure(c, c->d_bsend[k], c->cap_bsend[k], send)) != RRTE_OK) return r;
                 if ((r = ensure(c, c->d_brecv[k], c->cap_brecv[k], recv)) != RRTE_OK) return r;
             }
         }
-        // the slab is free once its previous batch has been gathered (usually long done)
-        HIPCHK(c, hipStreamWaitEvent(st, c->ev_batch[k], 0));
         hs.lap(2);
-        uint8_t* mine = c->d_bsend[k] + (size_t)b.n * slice;
-        if ((r = launch(c, s, &pp, rows, reinterpret_cast<uint32_t*>(mine), nullptr, st, kflags)) != RRTE_OK) return r;
-        hs.lap(3);
-        HIPCHK(c, hipEventRecord(b.ev_frame[b.n], st));
+        b.cam[b.n] = L.k.cam[0];
         b.full[b.n] = static_cast<uint32_t*>(d_full);
+        uint32_t i = 0;
+        while (i < b.nsrc && b.src[i] != st) ++i;
+        if (i == b.nsrc) b.src[b.nsrc++] = st;
         ++b.n;
+        hs.lap(3);
         if (b.n == b.cap && (r = flush_batch(c)) != RRTE_OK) return r;
     } else {
         if ((r = flush_batch(c)) != RRTE_OK) return r;  // keep every rank's collectives in issue order

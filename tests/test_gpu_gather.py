@@ -17,17 +17,20 @@ from rrte_amd.renderer import Context
 pytestmark = pytest.mark.gpu
 
 
-def _frames(n, w=320, h=200, alpha=None):
+def _frames(n, w=320, h=200, alpha=None, first=0):
     """`alpha`: None = the stock scene (every alpha byte 255: RGB24 slabs); "material" = one material
     with albedo alpha -150 (its pixels' alpha byte 127); "spp2" = 2 samples under a background alpha
-    of 0.2 (sky pixels 178).  The last two must fall back to RGBA8 slabs."""
+    of 0.2 (sky pixels 178).  The last two must fall back to RGBA8 slabs.  Frame i's camera is the
+    (first + i)-th of a fly-by."""
     out = []
-    for i in range(n):
+    for i in range(first, first + n):
         objs, lights, cam, cfg = scenes.sdf_showcase(w, h)
         cam.transform.position = vec3(0.0 + 0.7 * i, 8.0 - 0.3 * i, 20.0)
         cam.look_at((0, 2, 0))
         if alpha == "material":
             objs[3].material = LambertianMaterial(Color(0.2, 0.6, 0.9, -150.0))
+        elif alpha == "recolour":  # another scene, same slab format
+            objs[3].material = LambertianMaterial(Color(0.9, 0.3, 0.1, 1.0))
         elif alpha == "spp2":
             cfg.samples_per_pixel = 2
             cfg.background_color = Color(0.05, 0.05, 0.08, 0.2)
@@ -139,3 +142,42 @@ def test_gather_batch_arguments_and_size_change(monkeypatch):
     for i, o in enumerate(outs):
         assert np.array_equal(o.cpu().numpy().view(np.uint8), want[i]), f"frame {i}"
     ctx.close()
+
+
+def test_gather_batch_multi_frame_launches_and_changes(monkeypatch):
+    """A batch of 16 renders as two 8-frame launches (one camera per blockIdx.z); a scene change
+    (another material), a sampling change (2 spp) or a new camera set mid-batch closes or joins the
+    open batch as the header says, and every frame -- 26 of them, on two caller streams, the last
+    batch partial -- equals the plain render of its own scene and camera."""
+    import torch
+
+    monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    frames = _frames(18)
+    for sc_prm in _frames(3, first=18, alpha="recolour"):
+        frames.insert(11, sc_prm)  # scene change in the middle of the first batch
+    frames += _frames(3, first=21, alpha="spp2") + _frames(2, first=24)
+    ref = Context(0, jit=abi.JIT_OFF)
+    want = []
+    for sc, prm in frames:
+        buf = np.zeros(prm.width * prm.height * 4, dtype=np.uint8)
+        ref.check(ref.lib.rrte_hip_render(ref.h, sc.ref(), C.byref(prm), buf.ctypes.data_as(C.POINTER(C.c_uint8))))
+        want.append(buf)
+    ref.close()
+    assert not np.array_equal(want[0], want[1])  # every frame its own camera
+    for jit in (abi.JIT_ON, abi.JIT_OFF):
+        ctx = Context(0, jit=jit)
+        lib = ctx.lib
+        uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+        ctx.check(lib.rrte_hip_comm_unique_id(uid))
+        ctx.check(lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
+        ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 16))
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        outs = [torch.full((p.width * p.height,), -1, dtype=torch.int32, device="cuda") for _, p in frames]
+        for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
+            ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
+                                                        C.c_void_p(streams[i % 2].cuda_stream)))
+        ctx.check(lib.rrte_hip_synchronize(ctx.h))
+        for i, o in enumerate(outs):
+            got = o.cpu().numpy().view(np.uint8)
+            assert np.array_equal(got, want[i]), f"jit {jit} frame {i}: {(got != want[i]).sum()} bytes differ"
+        ctx.close()

@@ -37,7 +37,7 @@ sp = [C.c_void_p(s.cuda_stream) for s in streams]
 ref = sc.ref()
 
 
-def run(kind, flags=0, events=False, batch=1):
+def run(kind, flags=0, events=False, batch=1, one_stream=False):
     ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, batch))
     prm.flags = flags
     p = C.byref(prm)
@@ -47,7 +47,8 @@ def run(kind, flags=0, events=False, batch=1):
         if kind == "plain":
             st = lib.rrte_hip_render_async(ctx.h, ref, p, outs[i % F].data_ptr(), None, sp[i % F])
         else:
-            st = lib.rrte_hip_render_gather_async(ctx.h, ref, p, 0, outs[i % F].data_ptr(), sp[i % F])
+            st = lib.rrte_hip_render_gather_async(ctx.h, ref, p, 0, outs[i % F].data_ptr(),
+                                                  sp[0] if one_stream else sp[i % F])
         if st:
             ctx.check(st)
         if events:
@@ -67,10 +68,13 @@ def run(kind, flags=0, events=False, batch=1):
 
 
 for rep in range(2):
-    for name, kind, ev, batch in [("plain", "plain", False, 1), ("gather per frame", "gather", False, 1),
-                                  ("gather per frame+ev", "gather", True, 1), (f"gather batch {B}", "gather", False, B),
-                                  (f"gather batch {B}+ev", "gather", True, B)]:
-        enq, wall = run(kind, 0, ev, batch)
-        print(f"{name:22s} {W}x{H} F={F}: "
+    for name, kind, ev, batch, one in [("plain", "plain", False, 1, False),
+                                       ("gather per frame", "gather", False, 1, False),
+                                       ("gather per frame+ev", "gather", True, 1, False),
+                                       (f"gather batch {B}", "gather", False, B, False),
+                                       (f"gather batch {B} 1 stream", "gather", False, B, True),
+                                       (f"gather batch {B}+ev", "gather", True, B, False)]:
+        enq, wall = run(kind, 0, ev, batch, one)
+        print(f"{name:26s} {W}x{H} F={F}: "
               f"host {enq:6.1f} us/frame, wall {wall:6.1f} us/frame", flush=True)
 ctx.close()
