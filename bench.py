@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
                          "so one frame's tail overlaps the next frame's start (1 = strictly one after another); "
-                         "default 4 on one GPU, 8 per rank for N > 1 (tools/r02_inflight.sh)")
+                         "default 4 on one GPU (tools/r02_inflight.sh); N > 1: frames per gather batch, default 16")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
@@ -183,7 +183,7 @@ def main():
     if os.environ.get("RRTE_BENCH_DEVICE") is not None:
         local_rank = int(os.environ["RRTE_BENCH_DEVICE"])
     dist_on = world > 1
-    F = max(1, args.inflight if args.inflight is not None else (8 if world > 1 else 4))
+    F = max(1, args.inflight if args.inflight is not None else (16 if world > 1 else 4))
     if dist_on:
         dist.init_process_group("gloo")  # control plane only; the frame gather is RCCL inside librrte_hip
     torch.cuda.set_device(local_rank)
@@ -199,11 +199,13 @@ def main():
         cfg.jitter = "random"
     scene = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
-    # N > 1: frames render on their own streams and are gathered in batches of F (one ncclGather per F
-    # frames on the library's comm stream, rrte_hip_set_gather_batch): per-frame gathers chained
-    # across the F streams cost 50-90 us per rank-sized 1920x136 frame against 18 us for its render
-    # (tools/gather_variants.py, one GPU through a 1-rank communicator).  Every frame is still
-    # gathered to rank 0 and de-interleaved inside the timed region (flushed before its end).
+    # N > 1: frames are gathered in batches of F (rrte_hip_set_gather_batch): each batch renders in
+    # multi-frame launches (8 frames per launch) on the library's render streams and ONE ncclGather
+    # per batch on its comm stream moves it to rank 0.  Per-frame gathers chained across streams cost
+    # 50-90 us per rank-sized 1920x136 frame against 15 us for its render; batches of 16 cost 12 us
+    # per frame, gather and de-interleave included (tools/gather_variants.py, one GPU through a
+    # 1-rank communicator).  Every frame is still gathered to rank 0 and de-interleaved inside the
+    # timed region (flushed before its end).
     ctx = Context(local_rank, jit={"off": abi.JIT_OFF, "on": abi.JIT_ON, "auto": abi.JIT_AUTO}[args.jit])
     lib = ctx.lib
 

@@ -1553,37 +1553,18 @@ __global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, Cull
     ray_kernel_body<MODE, SceneView, false, CULL>(kp, sc, cl, out_rgba8, out_f32, counters);
 }
 
-// Root-side de-interleave after the RCCL gather: the gathered buffer holds each rank's packed
-// rows (rank-major, one `slice` of bytes per rank, `rows_cap` rows of RGBA8 or RGB24 each).
-// RGB24 slabs are expanded with alpha 255 (the host proved every alpha byte is 255).
-template <bool RGB24>
-__global__ __launch_bounds__(256) void deinterleave_kernel(const uint8_t* __restrict__ gathered,
-                                                           uint32_t* __restrict__ full, uint32_t width,
-                                                           uint32_t band_rows, uint32_t nranks, size_t slice) {
-    const uint32_t y = blockIdx.y;
-    const uint32_t band = y / band_rows, w = y - band * band_rows;
-    const uint32_t rank = band % nranks, local_band = band / nranks;
-    const uint32_t lr = local_band * band_rows + w;
-    constexpr uint32_t bpp = RGB24 ? 3u : 4u;
-    const uint8_t* src = gathered + (size_t)rank * slice + (size_t)lr * width * bpp;
-    uint32_t* dst = full + (size_t)y * width;
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < width; x += gridDim.x * blockDim.x) {
-        if constexpr (RGB24) {
-            const uint8_t* q = src + 3u * x;
-            dst[x] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | 0xFF000000u;
-        } else {
-            dst[x] = reinterpret_cast<const uint32_t*>(src)[x];
-        }
-    }
-}
-
-// Batched form (rrte_hip_set_gather_batch): the gathered buffer holds, per rank (rank_stride bytes
-// each), that rank's slices of `gridDim.z` frames back to back (frame_stride bytes each); frame z
-// goes to full[z].
+// Root-side de-interleave after the RCCL gather: the gathered buffer holds, per rank (rank_stride
+// bytes each), that rank's packed rows of `gridDim.z` frames back to back (frame_stride bytes each,
+// `rows_cap` rows of RGBA8 or RGB24 per frame); frame z goes to full[z] (one frame per launch for
+// per-frame gathers, a batch's frames for rrte_hip_set_gather_batch).  RGB24 slabs are expanded
+// with alpha 255 (the host proved every alpha byte is 255).  VEC4: each lane moves 4 pixels (three
+// dword loads for RGB24 or one dwordx4, one dwordx4 store) instead of 4 byte-wise pixels -- the
+// host picks it when the width is a multiple of 4 and every target is 16-byte aligned (the slab
+// strides are 256-byte aligned).  One workgroup row per image row, blockIdx.x strides the row.
 struct DeinterleaveTargets {
     uint32_t* full[16];
 };
-template <bool RGB24>
+template <bool RGB24, bool VEC4>
 __global__ __launch_bounds__(256) void deinterleave_batch_kernel(const uint8_t* __restrict__ gathered,
                                                                  DeinterleaveTargets t, uint32_t width,
                                                                  uint32_t band_rows, uint32_t nranks,
@@ -1596,12 +1577,35 @@ __global__ __launch_bounds__(256) void deinterleave_batch_kernel(const uint8_t* 
     const uint8_t* src = gathered + (size_t)rank * rank_stride + (size_t)blockIdx.z * frame_stride +
                          (size_t)lr * width * bpp;
     uint32_t* dst = t.full[blockIdx.z] + (size_t)y * width;
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < width; x += gridDim.x * blockDim.x) {
-        if constexpr (RGB24) {
-            const uint8_t* q = src + 3u * x;
-            dst[x] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | 0xFF000000u;
-        } else {
-            dst[x] = reinterpret_cast<const uint32_t*>(src)[x];
+    const uint32_t step = gridDim.x * blockDim.x;
+    if constexpr (VEC4) {
+        const uint32_t n4 = width >> 2;
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += step) {
+            uint4 o;
+            if constexpr (RGB24) {
+                // pixels 4i..4i+3 = bytes 12i..12i+11 = dwords 3i..3i+2 (little endian)
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(src) + 3u * i;
+                const uint32_t d0 = __builtin_nontemporal_load(q), d1 = __builtin_nontemporal_load(q + 1),
+                               d2 = __builtin_nontemporal_load(q + 2);
+                o.x = d0 | 0xFF000000u;
+                o.y = (d0 >> 24) | (d1 << 8) | 0xFF000000u;
+                o.z = (d1 >> 16) | (d2 << 16) | 0xFF000000u;
+                o.w = (d2 >> 8) | 0xFF000000u;
+            } else {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + i);
+                o = make_uint4(v.x, v.y, v.z, v.w);
+            }
+            reinterpret_cast<uint4*>(dst)[i] = o;
+        }
+    } else {
+        for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < width; x += step) {
+            if constexpr (RGB24) {
+                const uint8_t* q = src + 3u * x;
+                dst[x] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | 0xFF000000u;
+            } else {
+                dst[x] = reinterpret_cast<const uint32_t*>(src)[x];
+            }
         }
     }
 }

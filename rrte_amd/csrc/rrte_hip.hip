@@ -1204,6 +1204,27 @@ bool slab_rgb24(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_par
 // of them to the root in one ncclGather (each rank sends its frames' slices back to back) and
 // de-interleaves every frame into its caller buffer.  Every rank holds the same open batch (same
 // frames in the same order), so the collective matches.
+// De-interleave `n` gathered frames (ray_kernels.hpp deinterleave_batch_kernel) on `st`.
+static rrte_status deinterleave(rrte_ctx* c, hipStream_t st, const uint8_t* gathered, const DeinterleaveTargets& t,
+                                uint32_t n, uint32_t width, uint32_t height, uint32_t band, bool rgb24,
+                                size_t rank_stride, size_t frame_stride) {
+    bool vec4 = width % 4u == 0;
+    for (uint32_t j = 0; j < n; ++j) vec4 = vec4 && reinterpret_cast<uintptr_t>(t.full[j]) % 16u == 0;
+    const uint32_t per = vec4 ? 1024u : 256u;  // pixels one workgroup moves per pass
+    const dim3 dg(std::min((width + per - 1) / per, 8u), height, n), db(256);
+    const uint32_t nr = (uint32_t)c->nranks;
+    if (rgb24 && vec4)
+        hipLaunchKernelGGL((deinterleave_batch_kernel<true, true>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride);
+    else if (rgb24)
+        hipLaunchKernelGGL((deinterleave_batch_kernel<true, false>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride);
+    else if (vec4)
+        hipLaunchKernelGGL((deinterleave_batch_kernel<false, true>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride);
+    else
+        hipLaunchKernelGGL((deinterleave_batch_kernel<false, false>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride);
+    HIPCHK(c, hipGetLastError());
+    return RRTE_OK;
+}
+
 static rrte_status flush_batch(rrte_ctx* c) {
     rrte_ctx::Batch& b = c->batch;
     if (b.n == 0) return RRTE_OK;
@@ -1242,14 +1263,9 @@ static rrte_status flush_batch(rrte_ctx* c) {
     if (c->rank == b.root && !(c->env_diag_skip & 2u)) {
         DeinterleaveTargets t{};
         for (uint32_t j = 0; j < b.n; ++j) t.full[j] = b.full[j];
-        const dim3 dg((b.width + 255) / 256 < 8 ? (b.width + 255) / 256 : 8, b.height, b.n);
-        if (b.rgb24)
-            hipLaunchKernelGGL(deinterleave_batch_kernel<true>, dg, dim3(256), 0, c->comm_stream, c->d_brecv[k], t,
-                               b.width, b.band, (uint32_t)c->nranks, count, b.slice);
-        else
-            hipLaunchKernelGGL(deinterleave_batch_kernel<false>, dg, dim3(256), 0, c->comm_stream, c->d_brecv[k], t,
-                               b.width, b.band, (uint32_t)c->nranks, count, b.slice);
-        HIPCHK(c, hipGetLastError());
+        rrte_status r = deinterleave(c, c->comm_stream, c->d_brecv[k], t, b.n, b.width, b.height, b.band, b.rgb24,
+                                     count, b.slice);
+        if (r != RRTE_OK) return r;
     }
     hs.lap(6);
     HIPCHK(c, hipEventRecord(c->ev_batch[k], c->comm_stream));
@@ -1343,7 +1359,6 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         if (b.n == b.cap && (r = flush_batch(c)) != RRTE_OK) return r;
     } else {
         if ((r = flush_batch(c)) != RRTE_OK) return r;  // keep every rank's collectives in issue order
-        const dim3 dg((p->width + 255) / 256 < 8 ? (p->width + 255) / 256 : 8, p->height);
         if (!c->ev_gath[0])
             for (int i = 0; i < rrte_ctx::kSlabs; ++i)
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_gath[i], hipEventDisableTiming));
@@ -1374,13 +1389,9 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         NCCLCHK(c, ncclGather(mine, slab, slice, ncclUint8, root, c->comm, st));
         hs.lap(5);
         if (c->rank == root) {
-            if (rgb24)
-                hipLaunchKernelGGL(deinterleave_kernel<true>, dg, dim3(256), 0, st, slab, static_cast<uint32_t*>(d_full),
-                                   p->width, band, (uint32_t)c->nranks, slice);
-            else
-                hipLaunchKernelGGL(deinterleave_kernel<false>, dg, dim3(256), 0, st, slab, static_cast<uint32_t*>(d_full),
-                                   p->width, band, (uint32_t)c->nranks, slice);
-            HIPCHK(c, hipGetLastError());
+            DeinterleaveTargets t{};
+            t.full[0] = static_cast<uint32_t*>(d_full);
+            if ((r = deinterleave(c, st, slab, t, 1, p->width, p->height, band, rgb24, slice, 0)) != RRTE_OK) return r;
         }
         hs.lap(6);
         HIPCHK(c, hipEventRecord(c->ev_gath[slot], st));

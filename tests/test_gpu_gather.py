@@ -112,7 +112,7 @@ def test_gather_requires_comm_and_root_buffer(monkeypatch):
 def test_gather_batch_arguments_and_size_change(monkeypatch):
     """Batch sizes outside [1, 16] are rejected; flushing with no open batch is a no-op; a frame of
     another size closes the open batch (its frames are gathered first), and every frame of a stream
-    of alternating sizes still equals the plain render."""
+    of alternating sizes (one of them not a multiple of 4 wide) still equals the plain render."""
     import torch
 
     monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
@@ -125,7 +125,9 @@ def test_gather_batch_arguments_and_size_change(monkeypatch):
     assert lib.rrte_hip_set_gather_batch(ctx.h, 17) == abi.RRTE_INVALID_ARG
     ctx.check(lib.rrte_hip_flush(ctx.h))
     ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 4))
-    frames = [_frames(1, *((320, 200) if i % 3 else (160, 96)))[0] for i in range(8)]
+    # widths 320 / 160: 4-pixel de-interleave; 162: the per-pixel form
+    sizes = [(320, 200), (160, 96), (162, 90)]
+    frames = [_frames(1, *sizes[i % 3])[0] for i in range(9)]
     ref = Context(0, jit=abi.JIT_OFF)
     want = []
     for sc, prm in frames:
