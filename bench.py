@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
                          "so one frame's tail overlaps the next frame's start (1 = strictly one after another); "
-                         "default 4 on one GPU (tools/r02_inflight.sh); N > 1: frames per gather batch, default 16")
+                         "default 4 on one GPU (tools/r02_inflight.sh); N > 1: frames per gather batch, default 8")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
@@ -183,7 +183,13 @@ def main():
     if os.environ.get("RRTE_BENCH_DEVICE") is not None:
         local_rank = int(os.environ["RRTE_BENCH_DEVICE"])
     dist_on = world > 1
-    F = max(1, args.inflight if args.inflight is not None else (16 if world > 1 else 4))
+    # RRTE_BENCH_GATHER=1 (rehearsal on one GPU): the N > 1 frame path -- batched gathers through a
+    # 1-rank communicator (RRTE_FORCE_GATHER) -- at N=1; not a headline configuration
+    gath = dist_on or os.environ.get("RRTE_BENCH_GATHER") == "1"
+    if gath and not dist_on:
+        os.environ["RRTE_FORCE_GATHER"] = "1"
+    F = max(1, args.inflight if args.inflight is not None else (8 if gath else 4))
+    spin = os.environ.get("RRTE_BENCH_SPIN", "1") != "0"  # 0: close the timed region with the blocking sync only
     if dist_on:
         dist.init_process_group("gloo")  # control plane only; the frame gather is RCCL inside librrte_hip
     torch.cuda.set_device(local_rank)
@@ -202,20 +208,22 @@ def main():
     # N > 1: frames are gathered in batches of F (rrte_hip_set_gather_batch): each batch renders in
     # multi-frame launches (8 frames per launch) on the library's render streams and ONE ncclGather
     # per batch on its comm stream moves it to rank 0.  Per-frame gathers chained across streams cost
-    # 50-90 us per rank-sized 1920x136 frame against 15 us for its render; batches of 16 cost 12 us
-    # per frame, gather and de-interleave included (tools/gather_variants.py, one GPU through a
-    # 1-rank communicator).  Every frame is still gathered to rank 0 and de-interleaved inside the
-    # timed region (flushed before its end).
+    # 50-90 us per rank-sized 1920x136 frame against 15 us for its render; batches of 8 / 16 cost
+    # 14 / 12 us per frame, gather and de-interleave included (tools/gather_variants.py, one GPU
+    # through a 1-rank communicator, 400 frames); at the driver's 20 steps batches of 8 keep the
+    # last batch's gather (link-bound at N > 1) short.  Every frame is still gathered to rank 0 and
+    # de-interleaved inside the timed region (flushed before its end).
     ctx = Context(local_rank, jit={"off": abi.JIT_OFF, "on": abi.JIT_ON, "auto": abi.JIT_AUTO}[args.jit])
     lib = ctx.lib
 
-    if dist_on:
+    if gath:
         uid = torch.zeros(abi.UNIQUE_ID_BYTES, dtype=torch.uint8)
         if rank == 0:
             buf = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
             ctx.check(lib.rrte_hip_comm_unique_id(buf))
             uid.copy_(torch.tensor(list(buf), dtype=torch.uint8))
-        dist.broadcast(uid, 0)
+        if dist_on:
+            dist.broadcast(uid, 0)
         idb = (C.c_uint8 * abi.UNIQUE_ID_BYTES)(*uid.tolist())
         ctx.check(lib.rrte_hip_comm_init(ctx.h, world, rank, idb))
         ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, min(F, 16)))  # warm-up: the batched path
@@ -231,7 +239,7 @@ def main():
 
     def step(i=0):
         j = i % F
-        if dist_on:
+        if gath:
             # batched frames render on the library's own streams (multi-frame launches at the flush):
             # one caller stream keeps the batch's dependency on its callers to one event
             ctx.check(lib.rrte_hip_render_gather_async(ctx.h, scene.ref(), C.byref(prm), 0,
@@ -245,7 +253,7 @@ def main():
 
     # per-launch kernel duration (roofline): frames strictly one after another on one stream
     # (N > 1: each frame rendered and gathered on its own)
-    if dist_on:
+    if gath:
         ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 1))
     n_seq = min(args.steps, 20)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_seq)]
@@ -257,15 +265,26 @@ def main():
     launch_ms = [a.elapsed_time(b) for a, b in evs]
     ctx.check(lib.rrte_hip_synchronize(ctx.h))  # folds warm-up and sequential-pass shadow counts away
 
-    if dist_on:
+    if gath:
         ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, min(F, 16)))
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
-    if dist_on:
+    if gath:
         ctx.check(lib.rrte_hip_flush(ctx.h))  # the last, partial gather batch
+    if spin:
+        # poll for the end of the work (events on every stream the frames and the library used)
+        # before the closing synchronize: a blocking device synchronize wakes the host ~40 us after
+        # the last kernel ends (tools/r02_timeline2.sh); the work measured is the same
+        ends = [torch.cuda.Event() for _ in streams]
+        for e, s in zip(ends, streams):
+            e.record(s)
+        busy = C.c_uint32(1)
+        while busy.value or not all(e.query() for e in ends):
+            ctx.check(lib.rrte_hip_query(ctx.h, C.byref(busy)))
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if dist_on:
@@ -287,7 +306,7 @@ def main():
 
     # single-frame latency (enqueue -> frame complete on the device), D2H of the frame separately;
     # N > 1: each frame gathered on its own
-    if dist_on:
+    if gath:
         ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 1))
     lat = []
     for _ in range(5):
@@ -353,7 +372,8 @@ def main():
                 "workload": f"{args.scene} {W}x{H}, {args.mode}, spp={prm.samples_per_pixel}, max_depth={prm.max_depth}, "
                             + ("random jitter" if args.random else "pixel-centre jitter")
                             + (f", {args.band_rows}-row bands interleaved over {world} GPUs + RCCL gather to rank 0"
-                               f" in batches of {min(F, 16)} frames" if world > 1 else ""),
+                               f" in batches of {min(F, 16)} frames" if world > 1 else "")
+                            + (", REHEARSAL: gather path through a 1-rank communicator" if gath and not dist_on else ""),
                 "scene": args.scene, "width": W, "height": H, "mode": args.mode,
                 "primary_rays_per_frame": W * H * prm.samples_per_pixel,
                 "shadow_rays_per_frame": shadow // args.steps,

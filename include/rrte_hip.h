@@ -296,6 +296,10 @@ rrte_status rrte_hip_render_async(rrte_ctx* ctx, const rrte_scene_ir* scene,
                                   const rrte_render_params* params, void* d_out_rgba8,
                                   void* d_out_rgba32f, void* stream);
 rrte_status rrte_hip_synchronize(rrte_ctx* ctx);
+/* Non-blocking completion test of the work queued on the context's OWN streams (its default stream
+ * and the batched-gather render / comm streams; caller streams are the caller's to query): *busy = 1
+ * while any of it is still running, else 0.  Does not flush an open gather batch. */
+rrte_status rrte_hip_query(rrte_ctx* ctx, uint32_t* busy);
 
 rrte_status rrte_hip_stats(rrte_ctx* ctx, rrte_stats* out);
 

@@ -119,6 +119,7 @@ EXPORTS = {
     "rrte_hip_render_f32": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), _P, _P]),
     "rrte_hip_render_async": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), _P, _P, _P]),
     "rrte_hip_synchronize": (C.c_int, [_P]),
+    "rrte_hip_query": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
     "rrte_hip_stats": (C.c_int, [_P, C.POINTER(Stats)]),
     "rrte_hip_set_jit": (C.c_int, [_P, C.c_int]),
     "rrte_hip_jit_check": (C.c_int, [C.POINTER(SceneIR), C.c_int, C.c_char_p, C.c_size_t]),

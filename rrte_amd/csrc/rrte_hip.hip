@@ -1072,6 +1072,24 @@ rrte_status rrte_hip_synchronize(rrte_ctx* c) {
     return finish_frame(c);
 }
 
+rrte_status rrte_hip_query(rrte_ctx* c, uint32_t* busy) {
+    if (!c || !busy) return RRTE_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t ss[2 + rrte_ctx::kBatchSlabs] = {c->stream, c->comm_stream};
+    for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i) ss[2 + i] = c->render_stream[i];
+    *busy = 0;
+    for (hipStream_t s : ss) {
+        if (!s) continue;
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipErrorNotReady) {
+            *busy = 1;
+            return RRTE_OK;
+        }
+        HIPCHK(c, e);
+    }
+    return RRTE_OK;
+}
+
 rrte_status rrte_hip_set_jit(rrte_ctx* c, int mode) {
     if (!c) return RRTE_INVALID_ARG;
     if (mode < RRTE_JIT_OFF || mode > RRTE_JIT_AUTO) return fail(c, RRTE_INVALID_ARG, "unknown JIT mode %d", mode);
