@@ -68,6 +68,22 @@ __device__ __forceinline__ void for_each_prim(const S& sc, F&& f) {
         for (uint32_t i = 0; i < sc.num_prims; ++i) f(i);
     }
 }
+#ifndef RRTE_EXP_PRIM_ORDER
+#define RRTE_EXP_PRIM_ORDER 0
+#endif
+template <uint32_t I, uint32_t N, class F>
+__device__ __forceinline__ void static_for_rev(F& f) {
+    if constexpr (I < N) {
+        f(UC<N - 1u - I>{});
+        static_for_rev<I + 1, N>(f);
+    }
+}
+// EXPERIMENT: object order of the closest-hit (bit 0) / any-hit (bit 1) searches, reversed.
+template <int BIT, class S, class F>
+__device__ __forceinline__ void for_each_prim_exp(const S& sc, F&& f) {
+    if constexpr (S::kStatic && (RRTE_EXP_PRIM_ORDER & BIT)) static_for_rev<0, S::num_prims>(f);
+    else for_each_prim(sc, f);
+}
 // Scene record accessors.  For a static scene the record is copied in a
 // constant-expression context (constexpr local): device-side copies of
 // constexpr globals may be emitted as externally-initialised memory whose
@@ -854,14 +870,14 @@ __device__ __forceinline__ int closest_t(const S& sc, const Ray& r, float t_min,
     int idx = -1;
     best_t = kInf;
     best_sub = 0u;
-    for_each_prim(sc, [&](auto ii) {
+    for_each_prim_exp<1>(sc, [&](auto ii) {
         const uint32_t i = ii;
         if (i < 32u && !((pmask >> i) & 1u)) return;
         Hit h;
         h.sub = 0u;
         float tmax = (prim_at(sc, ii).kind == RRTE_PRIM_SDF && idx >= 0) ? best_t : kInf;
         if (intersect_at<false>(sc, ii, r, t_min, tmax, h)) {
-            if (idx < 0 || h.t < best_t) {
+            if (idx < 0 || h.t < best_t || (h.t == best_t && (int)i < idx)) {
                 best_t = h.t;
                 best_sub = h.sub;
                 idx = (int)i;
@@ -942,7 +958,7 @@ __device__ __forceinline__ bool any_hit_at(const S& sc, UC<I> ii, const Ray& r, 
 template <class S>
 __device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min, float t_max, uint64_t mask) {
     bool hit_any = false;
-    for_each_prim(sc, [&](auto ii) {
+    for_each_prim_exp<2>(sc, [&](auto ii) {
         const uint32_t i = ii;
         // one wave-uniform skip test: culled, or every lane already occluded (mask cleared)
         if (mask == 0 || (i < 64u && !((mask >> i) & 1ull))) return;
@@ -967,15 +983,31 @@ struct Cull {
     uint32_t n;                         // objects with a bound (culling needs n <= 64)
 };
 
+// Wave-wide min / max as a wave-uniform value: four DPP steps reduce each 16-lane row (quad_perm
+// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror -- every lane ends with its row's
+// value), then the four rows' lanes 0, 16, 32, 48 are read into scalars.  Exact for any order (min /
+// max); no LDS round trips (the ds_bpermute butterfly of __shfl_xor took six dependent ones).  Call
+// with all 64 lanes active.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
 __device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
+    v = fminf(v, dpp_f<0xB1>(v));
+    v = fminf(v, dpp_f<0x4E>(v));
+    v = fminf(v, dpp_f<0x141>(v));
+    v = fminf(v, dpp_f<0x140>(v));
+    return fminf(fminf(lane_f(v, 0), lane_f(v, 16)), fminf(lane_f(v, 32), lane_f(v, 48)));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-    return v;
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    v = fmaxf(v, dpp_f<0x140>(v));
+    return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 __device__ __forceinline__ bool cull_on(const Cull& cl) { return cl.bounds != nullptr && cl.n <= 64u; }
 
@@ -1004,7 +1036,14 @@ __device__ __forceinline__ HitBound wave_hit_bound(bool hit, f3 p, f3 n, float b
 // a non-finite hit point or normal, and directional lights whose direction is
 // not unit length (the sphere tracer's bound test assumes |d| = 1), are not
 // culled.  Wave-uniform inputs only: call with all 64 lanes active.
-__device__ __forceinline__ uint64_t shadow_cull(const Cull& cl, const HitBound& hb, const DLight& l) {
+// `bnd`: lane j's object bound (load_bound, once per wave for every light).  The projection
+// parameter uses the approximate reciprocal of |AB|^2: a relative error of ~1 ulp in t moves the
+// capsule point by ~|AB| t 2^-23, far inside the 1e-3 + 1e-4 * scale margin.
+__device__ __forceinline__ float4 load_bound(const Cull& cl) {
+    const uint32_t j = threadIdx.x & 63u;
+    return cl.bounds[j < cl.n ? j : 0u];
+}
+__device__ __forceinline__ uint64_t shadow_cull(const Cull& cl, const HitBound& hb, const DLight& l, float4 b) {
     if (!cull_on(cl) || hb.unsafe || l.kind == RRTE_LIGHT_AMBIENT) return ~0ull;
     if (!hb.any) return 0ull;
     const bool directional = l.kind == RRTE_LIGHT_DIRECTIONAL;
@@ -1014,22 +1053,17 @@ __device__ __forceinline__ uint64_t shadow_cull(const Cull& cl, const HitBound& 
     const f3 B = directional ? vsub(A, ld) : V(l.position[0], l.position[1], l.position[2]);
     const f3 AB = vsub(B, A);
     const float ab2 = vdot(AB, AB);
+    const float inv_ab2 = __builtin_amdgcn_rcpf(ab2);
     const float scale = fmaxf(fmaxf(fabsf(A.x), fabsf(A.y)), fmaxf(fabsf(A.z), fmaxf(fmaxf(fabsf(B.x), fabsf(B.y)), fabsf(B.z))));
     const float R = hb.r + hb.ext + 1e-3f + 1e-4f * scale;
     const uint32_t j = threadIdx.x & 63u;
-    bool cand = false;
-    if (j < cl.n) {
-        const float4 b = cl.bounds[j];
-        cand = true;
-        if (__builtin_isfinite(b.w) && ab2 > 0.0f) {
-            f3 P = V(b.x, b.y, b.z);
-            float t = vdot(vsub(P, A), AB) / ab2;
-            t = directional ? fmaxf(t, 0.0f) : clampf_(t, 0.0f, 1.0f);
-            f3 q = vsub(P, vadd(A, vmuls(AB, t)));
-            float rr = R + b.w;
-            cand = vdot(q, q) <= rr * rr * 1.0001f;
-        }
-    }
+    const f3 P = V(b.x, b.y, b.z);
+    float t = vdot(vsub(P, A), AB) * inv_ab2;
+    t = directional ? fmaxf(t, 0.0f) : clampf_(t, 0.0f, 1.0f);
+    const f3 q = vsub(P, vadd(A, vmuls(AB, t)));
+    const float rr = R + b.w;
+    const bool near = vdot(q, q) <= rr * rr * 1.0001f;
+    const bool cand = j < cl.n && (!(__builtin_isfinite(b.w) && ab2 > 0.0f) || near);
     return __ballot(cand);
 }
 
@@ -1319,18 +1353,22 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
     } else {
         HitBound hb{};
         hb.unsafe = true;  // no bounds table: every mask all-ones
-        if (cull_on(cl)) hb = wave_hit_bound(hit, h.p, h.n, bias);
+        float4 bnd{};
+        if (cull_on(cl)) {
+            bnd = load_bound(cl);
+            hb = wave_hit_bound(hit, h.p, h.n, bias);
+        }
         if constexpr (S::kStatic) {
             // all light masks first, at one converged point, then the shading
             uint64_t smask[S::num_lights ? S::num_lights : 1];
-            auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii)); };
+            auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii), bnd); };
             auto shade_one = [&](auto lii) { if (hit) shade(light_at(sc, lii), smask[(uint32_t)lii]); };
             static_for<0, S::num_lights>(cull_one);
             static_for<0, S::num_lights>(shade_one);
         } else {
 #pragma unroll 1
             for (uint32_t li = 0; li < sc.num_lights; ++li) {
-                const uint64_t sm = shadow_cull(cl, hb, sc.lights[li]);
+                const uint64_t sm = shadow_cull(cl, hb, sc.lights[li], bnd);
                 if (hit) shade(sc.lights[li], sm);
             }
         }
@@ -1524,9 +1562,13 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     }
     if (MODE != RRTE_MODE_REFCOMPAT) {
         // wave-reduce the shadow-ray count, one atomic per wave
-        uint32_t v = nshadow;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        uint32_t v = nshadow;  // (DPP row sums, then the four rows' lanes: as wave_min)
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+        v = (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+            (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
         // 256 counter shards, one 128-B line each: same-address atomics from
         // every wave of the grid would serialise at the memory side.
         if (lane == 0 && v) {
