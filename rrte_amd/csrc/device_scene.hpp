@@ -105,7 +105,7 @@ constexpr uint32_t kFlagSlabRgb24 = 1u << 31;
 struct f3 { float x, y, z; };
 
 __device__ __forceinline__ f3 V(float x, float y, float z) { return f3{x, y, z}; }
-// Correctly rounded f32 sqrt (Rust f32::sqrt), 6 VALU ops instead of the compiler's 16.
+// Correctly rounded f32 sqrt (Rust f32::sqrt), 7 VALU ops with its guard instead of the compiler's 16.
 // Verified bit-identical to __builtin_sqrtf over all 2^32 inputs on gfx950 (rrte_hip_fpcheck,
 // tests/test_gpu_fpexact.py).  (Round 1's form -- the neighbour of v_sqrt_f32 whose residual
 // x - s*(s -/+ ulp) changes sign, guarded below 2^-96 -- took 11.)
@@ -115,16 +115,18 @@ __device__ __forceinline__ f3 V(float x, float y, float z) { return f3{x, y, z};
 __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_amdgcn_sqrtf(x); }
 #else
 __device__ __forceinline__ float sqrt_rn(float x) {
-    // one residual correction: s = v_sqrt_f32(x) (faithful), e = x - s*s exactly (one fma), and
-    // r = RN(s + e * h) with h = 0.5 * v_rsq_f32(x) ~ 1/(2 sqrt x): 5 VALU ops (two of them
-    // transcendental) against 9 for the two-sided neighbour test.  Correctly rounded for every x in
-    // [2^-96, FLT_MAX] (tools/fpexact/sqrt_markstein.hip: below it the residual underflows); every
-    // other x -- tiny, zero, denormal, negative, infinite, NaN -- takes the compiler's sequence in a
-    // divergent branch no real scene takes, chosen by one unsigned range test on the bits (positive
-    // floats order like their bit patterns; negatives and NaNs fall outside).
-    const float s = __builtin_amdgcn_sqrtf(x);
+    // one residual correction from a single transcendental: y = v_rsq_f32(x), s = x * y (faithful),
+    // e = x - s*s exactly (one fma), r = RN(s + e * h) with h = 0.5 * y ~ 1/(2 sqrt x): 5 VALU ops,
+    // ONE of them transcendental (8 issue cycles against 4 for an fma; s from v_sqrt_f32 plus h from
+    // v_rsq_f32 took two).  Correctly rounded for every x in [2^-96, FLT_MAX] (tools/fpexact/
+    // sqrt_markstein.hip, candidate M3: only 0 and inf fail, both outside; below 2^-96 the residual
+    // underflows); every other x -- tiny, zero, denormal, negative, infinite, NaN -- takes the
+    // compiler's sequence in a divergent branch no real scene takes, chosen by one unsigned range
+    // test on the bits (positive floats order like their bit patterns; negatives and NaNs fall outside).
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s = x * y;
     const float e = __builtin_fmaf(-s, s, x);
-    float r = __builtin_fmaf(e, 0.5f * __builtin_amdgcn_rsqf(x), s);
+    float r = __builtin_fmaf(e, 0.5f * y, s);
     constexpr uint32_t kLo = 0x0F800000u, kInf = 0x7F800000u;  // bits of 2^-96 and +inf
     if (__builtin_expect(__float_as_uint(x) - kLo >= kInf - kLo, 0)) r = __builtin_sqrtf(x);
     return r;
