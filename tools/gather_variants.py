@@ -67,7 +67,7 @@ def run(kind, flags=0, events=False, batch=1, one_stream=False):
     return 1e6 * (t1 - t0) / N, 1e6 * (t2 - t0) / N
 
 
-for rep in range(2):
+for rep in range(int(os.environ.get("GV_REPS", "2"))):
     for name, kind, ev, batch, one in [("plain", "plain", False, 1, False),
                                        ("gather per frame", "gather", False, 1, False),
                                        ("gather per frame+ev", "gather", True, 1, False),
