@@ -983,32 +983,32 @@ struct Cull {
     uint32_t n;                         // objects with a bound (culling needs n <= 64)
 };
 
-// Wave-wide min / max as a wave-uniform value: four DPP steps reduce each 16-lane row (quad_perm
-// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_mirror -- every lane ends with its row's
-// value), then the four rows' lanes 0, 16, 32, 48 are read into scalars.  Exact for any order (min /
-// max); no LDS round trips (the ds_bpermute butterfly of __shfl_xor took six dependent ones).  Call
-// with all 64 lanes active.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+// Wave-wide min / max as a wave-uniform value, on order-preserving integer keys of the floats
+// (key(f) = bits ^ ((bits >> 31) & 0x7fffffff): signed-integer order = float order, -0 < +0, and the
+// map is its own inverse): four DPP steps reduce each 16-lane row (quad_perm [1,0,3,2], quad_perm
+// [2,3,0,1], row_half_mirror, row_mirror -- each a v_min_i32 / v_max_i32 with its DPP source, where
+// a float min needs a canonicalising v_max_f32 per operand and a separate v_mov_b32_dpp), then the
+// four rows' lanes 0, 16, 32, 48 are read into SGPRs and combined on the scalar unit.  No LDS round
+// trips (the ds_bpermute butterfly of __shfl_xor took six dependent ones).  Call with all 64 lanes
+// active; NaN-free inputs (the callers select +/-inf for unused lanes).
+__device__ __forceinline__ int fkey(float f) {
+    const int b = __float_as_int(f);
+    return b ^ ((b >> 31) & 0x7fffffff);
 }
-__device__ __forceinline__ float lane_f(float v, int lane) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+__device__ __forceinline__ float funkey(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+template <bool MAX>
+__device__ __forceinline__ int wave_reduce_key(int v) {
+    auto op = [](int a, int b) { return MAX ? (a > b ? a : b) : (a < b ? a : b); };
+    v = op(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true));
+    v = op(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true));
+    v = op(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true));
+    v = op(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true));
+    const int r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const int r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    return op(op(r0, r1), op(r2, r3));
 }
-__device__ __forceinline__ float wave_min(float v) {
-    v = fminf(v, dpp_f<0xB1>(v));
-    v = fminf(v, dpp_f<0x4E>(v));
-    v = fminf(v, dpp_f<0x141>(v));
-    v = fminf(v, dpp_f<0x140>(v));
-    return fminf(fminf(lane_f(v, 0), lane_f(v, 16)), fminf(lane_f(v, 32), lane_f(v, 48)));
-}
-__device__ __forceinline__ float wave_max(float v) {
-    v = fmaxf(v, dpp_f<0xB1>(v));
-    v = fmaxf(v, dpp_f<0x4E>(v));
-    v = fmaxf(v, dpp_f<0x141>(v));
-    v = fmaxf(v, dpp_f<0x140>(v));
-    return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
-}
+__device__ __forceinline__ float wave_min(float v) { return funkey(wave_reduce_key<false>(fkey(v))); }
+__device__ __forceinline__ float wave_max(float v) { return funkey(wave_reduce_key<true>(fkey(v))); }
 __device__ __forceinline__ bool cull_on(const Cull& cl) { return cl.bounds != nullptr && cl.n <= 64u; }
 
 // Bounding sphere of the wave's shading points (lanes with `hit`).
@@ -1017,8 +1017,15 @@ struct HitBound { f3 c; float r, ext; bool any, unsafe; };
 __device__ __forceinline__ HitBound wave_hit_bound(bool hit, f3 p, f3 n, float bias) {
     const bool use = hit && finite3(p) && finite3(n);
     const float ext = bias * vlen(n);
-    float lx = wave_min(use ? p.x : kInf), ly = wave_min(use ? p.y : kInf), lz = wave_min(use ? p.z : kInf);
-    float hx = wave_max(use ? p.x : -kInf), hy = wave_max(use ? p.y : -kInf), hz = wave_max(use ? p.z : -kInf);
+    // min and max of one coordinate share its key; unused lanes take the keys of +inf / -inf
+    constexpr int kPosInf = 0x7f800000, kNegInf = (int)(0xff800000u ^ 0x7fffffffu);
+    const int kx = fkey(p.x), ky = fkey(p.y), kz = fkey(p.z);
+    const float lx = funkey(wave_reduce_key<false>(use ? kx : kPosInf));
+    const float ly = funkey(wave_reduce_key<false>(use ? ky : kPosInf));
+    const float lz = funkey(wave_reduce_key<false>(use ? kz : kPosInf));
+    const float hx = funkey(wave_reduce_key<true>(use ? kx : kNegInf));
+    const float hy = funkey(wave_reduce_key<true>(use ? ky : kNegInf));
+    const float hz = funkey(wave_reduce_key<true>(use ? kz : kNegInf));
     HitBound b;
     b.any = lx <= hx;
     b.unsafe = __any(hit && !use);
@@ -1065,6 +1072,70 @@ __device__ __forceinline__ uint64_t shadow_cull(const Cull& cl, const HitBound& 
     const bool near = vdot(q, q) <= rr * rr * 1.0001f;
     const bool cand = j < cl.n && (!(__builtin_isfinite(b.w) && ab2 > 0.0f) || near);
     return __ballot(cand);
+}
+
+// All lights' masks in one lane-parallel pass (scene-specialised kernels with objects x lights <= 64):
+// lane L tests object j = L mod n against light l = L div n's capsule -- the same test as
+// shadow_cull, whose per-light wave-uniform prologue (capsule axis, |AB|^2, its reciprocal, the
+// margin) every light repeated on all 64 lanes -- and one ballot carries every light's n bits.
+// Lights shadow_cull never culls (ambient; directional with a non-unit direction) get all-ones.
+template <class S>
+__device__ __forceinline__ void shadow_cull_lanes(const Cull& cl, const HitBound& hb, uint64_t* smask) {
+    constexpr uint32_t n = S::num_prims, nl = S::num_lights;
+    static_assert(n * nl <= 64u && n > 0u, "one lane per (light, object)");
+    auto cullable = [](auto lii) {
+        constexpr DLight L = S::lights[(uint32_t)lii];
+        if constexpr (L.kind == RRTE_LIGHT_AMBIENT) return false;
+        else if constexpr (L.kind == RRTE_LIGHT_DIRECTIONAL) {
+            constexpr float d2 = (L.direction[0] * L.direction[0] + L.direction[1] * L.direction[1]) +
+                                 L.direction[2] * L.direction[2];
+            return (d2 - 1.0f <= 1e-3f) && (1.0f - d2 <= 1e-3f);
+        } else {
+            return true;
+        }
+    };
+    if (!cull_on(cl) || hb.unsafe || !hb.any) {
+        auto fill = [&](auto lii) { smask[(uint32_t)lii] = (cullable(lii) && cull_on(cl) && !hb.unsafe) ? 0ull : ~0ull; };
+        static_for<0, nl>(fill);
+        return;
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t l = lane / n, j = lane - l * n;
+    const f3 A = hb.c;
+    f3 B = A;
+    bool directional = false;
+    auto pick = [&](auto lii) {
+        constexpr DLight L = S::lights[(uint32_t)lii];
+        if (l == (uint32_t)lii) {
+            if constexpr (L.kind == RRTE_LIGHT_DIRECTIONAL) {
+                B = vsub(A, V(L.direction[0], L.direction[1], L.direction[2]));
+                directional = true;
+            } else {
+                B = V(L.position[0], L.position[1], L.position[2]);
+            }
+        }
+    };
+    static_for<0, nl>(pick);
+    const f3 AB = vsub(B, A);
+    const float ab2 = vdot(AB, AB);
+    const float inv_ab2 = __builtin_amdgcn_rcpf(ab2);
+    const float scale = fmaxf(fmaxf(fabsf(A.x), fabsf(A.y)), fmaxf(fabsf(A.z), fmaxf(fmaxf(fabsf(B.x), fabsf(B.y)), fabsf(B.z))));
+    const float R = hb.r + hb.ext + 1e-3f + 1e-4f * scale;
+    const float4 b = cl.bounds[j < cl.n ? j : 0u];
+    const f3 P = V(b.x, b.y, b.z);
+    float t = vdot(vsub(P, A), AB) * inv_ab2;
+    t = directional ? fmaxf(t, 0.0f) : clampf_(t, 0.0f, 1.0f);
+    const f3 q = vsub(P, vadd(A, vmuls(AB, t)));
+    const float rr = R + b.w;
+    const bool near = vdot(q, q) <= rr * rr * 1.0001f;
+    const bool cand = l < nl && j < cl.n && (!(__builtin_isfinite(b.w) && ab2 > 0.0f) || near);
+    const uint64_t m = __ballot(cand);
+    constexpr uint64_t kBits = n >= 64u ? ~0ull : ((1ull << n) - 1ull);
+    auto split = [&](auto lii) {
+        constexpr uint32_t li = (uint32_t)lii;
+        smask[li] = cullable(lii) ? ((m >> (li * n)) & kBits) : ~0ull;
+    };
+    static_for<0, nl>(split);
 }
 
 // --------------------------------------------------------------- lighting
@@ -1353,19 +1424,21 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
     } else {
         HitBound hb{};
         hb.unsafe = true;  // no bounds table: every mask all-ones
-        float4 bnd{};
-        if (cull_on(cl)) {
-            bnd = load_bound(cl);
-            hb = wave_hit_bound(hit, h.p, h.n, bias);
-        }
+        if (cull_on(cl)) hb = wave_hit_bound(hit, h.p, h.n, bias);
         if constexpr (S::kStatic) {
             // all light masks first, at one converged point, then the shading
             uint64_t smask[S::num_lights ? S::num_lights : 1];
-            auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii), bnd); };
+            if constexpr (S::num_lights > 0 && S::num_prims * S::num_lights <= 64u) {
+                shadow_cull_lanes<S>(cl, hb, smask);
+            } else {
+                const float4 bnd = cull_on(cl) ? load_bound(cl) : float4{};
+                auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii), bnd); };
+                static_for<0, S::num_lights>(cull_one);
+            }
             auto shade_one = [&](auto lii) { if (hit) shade(light_at(sc, lii), smask[(uint32_t)lii]); };
-            static_for<0, S::num_lights>(cull_one);
             static_for<0, S::num_lights>(shade_one);
         } else {
+            const float4 bnd = cull_on(cl) ? load_bound(cl) : float4{};
 #pragma unroll 1
             for (uint32_t li = 0; li < sc.num_lights; ++li) {
                 const uint64_t sm = shadow_cull(cl, hb, sc.lights[li], bnd);

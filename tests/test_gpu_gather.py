@@ -183,3 +183,50 @@ def test_gather_batch_multi_frame_launches_and_changes(monkeypatch):
             got = o.cpu().numpy().view(np.uint8)
             assert np.array_equal(got, want[i]), f"jit {jit} frame {i}: {(got != want[i]).sum()} bytes differ"
         ctx.close()
+
+
+def test_query_reports_batched_work_done(monkeypatch):
+    """rrte_hip_query: after a flush, polling until the context's own streams are idle is enough for
+    every batched frame to be complete (the frames render and gather on the context's streams) --
+    no device synchronisation before the outputs are read."""
+    import torch
+
+    monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    frames = _frames(6)
+    ref = Context(0, jit=abi.JIT_ON)
+    want = []
+    for sc, prm in frames:
+        buf = np.zeros(prm.width * prm.height * 4, dtype=np.uint8)
+        ref.check(ref.lib.rrte_hip_render(ref.h, sc.ref(), C.byref(prm), buf.ctypes.data_as(C.POINTER(C.c_uint8))))
+        want.append(buf)
+    ref.close()
+    ctx = Context(0, jit=abi.JIT_ON)
+    lib = ctx.lib
+    busy = C.c_uint32(7)
+    ctx.check(lib.rrte_hip_query(ctx.h, C.byref(busy)))
+    assert busy.value == 0  # nothing issued yet
+    assert lib.rrte_hip_query(ctx.h, None) == abi.RRTE_INVALID_ARG
+    uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+    ctx.check(lib.rrte_hip_comm_unique_id(uid))
+    ctx.check(lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
+    ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 4))
+    stream = torch.cuda.Stream()
+    outs = [torch.full((p.width * p.height,), -1, dtype=torch.int32, device="cuda") for _, p in frames]
+    torch.cuda.synchronize()
+    for (sc, prm), o in zip(frames, outs):
+        ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
+                                                    C.c_void_p(stream.cuda_stream)))
+    ctx.check(lib.rrte_hip_flush(ctx.h))
+    busy.value = 1
+    while busy.value:
+        ctx.check(lib.rrte_hip_query(ctx.h, C.byref(busy)))
+    host = [torch.empty_like(o, device="cpu") for o in outs]
+    side = torch.cuda.Stream()  # a stream that never waited on the library's work
+    with torch.cuda.stream(side):
+        for h, o in zip(host, outs):
+            h.copy_(o)
+    side.synchronize()
+    for i, h in enumerate(host):
+        assert np.array_equal(h.numpy().view(np.uint8), want[i]), f"frame {i}"
+    ctx.check(lib.rrte_hip_synchronize(ctx.h))
+    ctx.close()
