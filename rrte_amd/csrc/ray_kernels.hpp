@@ -1011,28 +1011,31 @@ __device__ __forceinline__ float wave_min(float v) { return funkey(wave_reduce_k
 __device__ __forceinline__ float wave_max(float v) { return funkey(wave_reduce_key<true>(fkey(v))); }
 __device__ __forceinline__ bool cull_on(const Cull& cl) { return cl.bounds != nullptr && cl.n <= 64u; }
 
-// Bounding sphere of the wave's shading points (lanes with `hit`).
-// `ext` = the lane's shadow-origin offset |n|*bias (normals need not be unit).
+// Bounding sphere of the wave's shading points (lanes with `hit`) grown by each lane's shadow-origin
+// offset |n|*bias (normals need not be unit): centred on one used lane's point (the tile's centre
+// lane 36 when it is used, else the first used lane), radius = max over used lanes of
+// |p - c| + offset -- one wave reduction (the bounding box took seven: min and max of three
+// coordinates and the largest offset).  `ext` stays 0 (folded into r).
 struct HitBound { f3 c; float r, ext; bool any, unsafe; };
 __device__ __forceinline__ HitBound wave_hit_bound(bool hit, f3 p, f3 n, float bias) {
     const bool use = hit && finite3(p) && finite3(n);
-    const float ext = bias * vlen(n);
-    // min and max of one coordinate share its key; unused lanes take the keys of +inf / -inf
-    constexpr int kPosInf = 0x7f800000, kNegInf = (int)(0xff800000u ^ 0x7fffffffu);
-    const int kx = fkey(p.x), ky = fkey(p.y), kz = fkey(p.z);
-    const float lx = funkey(wave_reduce_key<false>(use ? kx : kPosInf));
-    const float ly = funkey(wave_reduce_key<false>(use ? ky : kPosInf));
-    const float lz = funkey(wave_reduce_key<false>(use ? kz : kPosInf));
-    const float hx = funkey(wave_reduce_key<true>(use ? kx : kNegInf));
-    const float hy = funkey(wave_reduce_key<true>(use ? ky : kNegInf));
-    const float hz = funkey(wave_reduce_key<true>(use ? kz : kNegInf));
     HitBound b;
-    b.any = lx <= hx;
+    b.ext = 0.0f;
     b.unsafe = __any(hit && !use);
-    b.c = V((lx + hx) * 0.5f, (ly + hy) * 0.5f, (lz + hz) * 0.5f);
-    f3 d = V(hx - lx, hy - ly, hz - lz);
-    b.r = 0.5f * sqrt_rn(vdot(d, d));
-    b.ext = wave_max(use ? ext : 0.0f);
+    const uint64_t used = __ballot(use);
+    b.any = used != 0ull;
+    if (!b.any) {
+        b.c = V(0.0f, 0.0f, 0.0f);
+        b.r = 0.0f;
+        return b;
+    }
+    const int src = ((used >> 36) & 1ull) ? 36 : (int)__builtin_ctzll(used);
+    b.c = V(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), src)),
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), src)),
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), src)));
+    const f3 d = vsub(p, b.c);
+    const float reach = sqrt_rn(vdot(d, d)) + bias * vlen(n);  // both >= 0, NaN-free on used lanes
+    b.r = __int_as_float(wave_reduce_key<true>(use ? __float_as_int(reach) : 0));  // keys of floats >= 0 = bits
     return b;
 }
 
