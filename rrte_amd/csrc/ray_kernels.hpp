@@ -477,6 +477,15 @@ __device__ __forceinline__ bool isect_sphere(const DPrim& pr, const Ray& r, floa
     return true;
 }
 
+// Hit attributes of a sphere hit found by the search at t (= the root isect_sphere returns for the same
+// ray with t_max = INFINITY): the point and normal exactly as isect_sphere builds them, without
+// solving the quadratic again.
+__device__ __forceinline__ void sphere_attributes(const DPrim& pr, const Ray& r, float t, Hit& out) {
+    const f3 ctr = V(pr.p[0], pr.p[1], pr.p[2]);
+    const f3 p = ray_at(r, t);
+    hit_new(out, t, p, vdivs(vsub(p, ctr), pr.p[3]), r);
+}
+
 template <bool NEED_HIT>
 __device__ __forceinline__ bool isect_plane(const DPrim& pr, const Ray& r, float t_min, float t_max, Hit& out) {  // primitives.rs:133-149
     f3 pt = V(pr.p[0], pr.p[1], pr.p[2]), n = V(pr.p[4], pr.p[5], pr.p[6]);
@@ -899,6 +908,7 @@ __device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray
     const DPrim& pr = sc.prims[i];
     if (pr.kind == RRTE_PRIM_SDF) sdf_hit_attributes(SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t, out);
     else if (pr.kind == RRTE_PRIM_MESH) mesh_tri_hit(sc.mesh, sub, r, t_min, kInf, out);
+    else if (pr.kind == RRTE_PRIM_SPHERE) sphere_attributes(pr, r, t, out);
     else intersect_at<true>(sc, i, r, t_min, kInf, out);
 }
 template <class S, uint32_t I>
@@ -909,6 +919,8 @@ __device__ __forceinline__ void attributes_at(const S& sc, UC<I> ii, const Ray& 
         sdf_hit_attributes(SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t, out);
     else if constexpr (pr.kind == RRTE_PRIM_MESH)
         mesh_tri_hit(sc.mesh, sub, r, t_min, kInf, out);
+    else if constexpr (pr.kind == RRTE_PRIM_SPHERE)
+        sphere_attributes(pr, r, t, out);
     else
         intersect_at<true>(sc, ii, r, t_min, kInf, out);
 }
@@ -936,11 +948,12 @@ __device__ __forceinline__ void hit_attributes(const S& sc, const Ray& r, float 
 }
 
 template <class S>
-__device__ __forceinline__ int closest_hit(const S& sc, const Ray& r, float t_min, Hit& best, uint32_t pmask = ~0u) {
+__device__ __forceinline__ int closest_hit(const S& sc, const Ray& r, float t_min, Hit& best, uint32_t pmask = ~0u,
+                                           bool attributes = true) {
     float t;
     uint32_t sub;
     int idx = closest_t(sc, r, t_min, t, sub, pmask);
-    hit_attributes(sc, r, t_min, idx, t, sub, best);
+    if (attributes) hit_attributes(sc, r, t_min, idx, t, sub, best);
     return idx;
 }
 
@@ -956,14 +969,15 @@ __device__ __forceinline__ bool any_hit_at(const S& sc, UC<I> ii, const Ray& r, 
 
 // Any hit in [t_min, t_max] (LAMBERT_SHADOW shadow rays).
 template <class S>
-__device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min, float t_max, uint64_t mask) {
+__device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min, float t_max, uint64_t mask,
+                                         int self = -1) {
     bool hit_any = false;
     for_each_prim_exp<2>(sc, [&](auto ii) {
         const uint32_t i = ii;
         // one wave-uniform skip test: culled, or every lane already occluded (mask cleared)
         if (mask == 0 || (i < 64u && !((mask >> i) & 1ull))) return;
         Hit h;
-        if (!hit_any && any_hit_at(sc, ii, r, t_min, t_max, h)) hit_any = true;
+        if (!hit_any && (int)i != self && any_hit_at(sc, ii, r, t_min, t_max, h)) hit_any = true;
         if (__all(hit_any)) mask = 0;
     });
     return hit_any;
@@ -1018,7 +1032,11 @@ __device__ __forceinline__ bool cull_on(const Cull& cl) { return cl.bounds != nu
 // coordinates and the largest offset).  `ext` stays 0 (folded into r).
 struct HitBound { f3 c; float r, ext; bool any, unsafe; };
 __device__ __forceinline__ HitBound wave_hit_bound(bool hit, f3 p, f3 n, float bias) {
-    const bool use = hit && finite3(p) && finite3(n);
+    // the pre-pass only has to be conservative, so it uses cheap bounds: one finiteness test on a sum
+    // (a NaN or infinite term, or an overflowing sum, marks the lane unusable -- the wave is then
+    // not culled), the 1-ulp hardware square root scaled up by 2^-20, and the offset bound
+    // bias * |n|_1 >= bias * |n|_2; the cull margin (1e-3 + 1e-4 * scale) dwarfs their rounding
+    const bool use = hit && __builtin_isfinite(((p.x + p.y) + (p.z + n.x)) + (n.y + n.z));
     HitBound b;
     b.ext = 0.0f;
     b.unsafe = __any(hit && !use);
@@ -1034,7 +1052,8 @@ __device__ __forceinline__ HitBound wave_hit_bound(bool hit, f3 p, f3 n, float b
             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), src)),
             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), src)));
     const f3 d = vsub(p, b.c);
-    const float reach = sqrt_rn(vdot(d, d)) + bias * vlen(n);  // both >= 0, NaN-free on used lanes
+    const float reach = __builtin_amdgcn_sqrtf(vdot(d, d)) * 1.000001f +
+                        bias * ((fabsf(n.x) + fabsf(n.y)) + fabsf(n.z));  // >= 0, NaN-free on used lanes
     b.r = __int_as_float(wave_reduce_key<true>(use ? __float_as_int(reach) : 0));  // keys of floats >= 0 = bits
     return b;
 }
@@ -1383,7 +1402,8 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
     Col out{0.0f, 0.0f, 0.0f, 1.0f};
     if (kp.max_depth == 0) return out;
     Hit h;
-    const int idx = closest_hit(sc, r, live ? kp.t_min : kInf, h, pmask);  // idle lanes find nothing
+    // RRTE_DEBUG bit 7 (timing diagnostics only, with bit 1): the closest-hit search without hit attributes
+    const int idx = closest_hit(sc, r, live ? kp.t_min : kInf, h, pmask, !(kp.debug & 128u));  // idle lanes find nothing
     const DMaterial* m = idx >= 0 ? material_of(sc, idx) : nullptr;
     const bool hit = m != nullptr;
     if (idx < 0) out = Col{kp.bg[0], kp.bg[1], kp.bg[2], kp.bg[3]};
@@ -1414,7 +1434,8 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
         if (ndl > 0.0f && k.att > 0.0f) {
             ++nshadow;
             Ray sr = ray_new(vadd(h.p, vmuls(h.n, bias)), k.dir);
-            if ((kp.debug & 1u) || !occluded(sc, sr, bias, k.dist, smask)) {
+            // RRTE_DEBUG bit 6 (timing diagnostics only, wrong images): skip the object the ray starts on
+            if ((kp.debug & 1u) || !occluded(sc, sr, bias, k.dist, smask, (kp.debug & 64u) ? idx : -1)) {
                 float f = k.att * ndl;
                 cr = cr + ar * (k.cr * f);
                 cg = cg + ag * (k.cg * f);
