@@ -384,12 +384,58 @@ __device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float
     return hb > 0.0f && cc > 0.0f && a >= 0.25f && t_min >= 0x1p-57f;
 }
 
+// Is the postfix program a convex, 1-Lipschitz function of p?  Convex leaves (exact SDFs of convex
+// solids -- the signed distance of a convex set is a supremum of affine functions -- and the prism's
+// max of 1-Lipschitz convex terms) and intersections (max) of such; union, difference, smooth ops,
+// the other leaves and every deformer are not.  Evaluated at compile time for the scene-specialised
+// kernels (sdf_march CONVEX).
+#ifndef RRTE_SECANT_EXIT
+#define RRTE_SECANT_EXIT 2
+#endif
+constexpr int kSecantExit = RRTE_SECANT_EXIT;  // 0 off, 1 any-hit marches, 2 closest-hit marches too
+constexpr bool sdf_convex(const rrte_sdf_node* n, uint32_t count) {
+    bool st[RRTE_SDF_MAX_STACK] = {};
+    uint32_t sp = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        const uint32_t op = n[i].op;
+        if (op < 32u) {
+            if (sp >= RRTE_SDF_MAX_STACK) return false;
+            // (box, cylinder and capsule stay convex for any sizes: a degenerate one drops the
+            // inside term; the cone formula is the exact SDF only for radius, height > 0)
+            st[sp++] = op == RRTE_SDF_SPHERE || op == RRTE_SDF_BOX || op == RRTE_SDF_CYLINDER ||
+                       op == RRTE_SDF_PRISM || op == RRTE_SDF_CAPSULE ||
+                       (op == RRTE_SDF_CONE && n[i].f[3] > 0.0f && n[i].f[4] > 0.0f);
+        } else if (op < 64u) {
+            if (sp < 2u) return false;
+            const bool c = op == RRTE_SDF_INTERSECTION && st[sp - 1] && st[sp - 2];
+            sp -= 2;
+            st[sp++] = c;
+        } else {
+            return false;  // deformers (and their point-stack pops)
+        }
+    }
+    return sp == 1u && st[0];
+}
+
 // SDFObject::intersect, search part -- sphere tracing inside the object's
 // bounding sphere (build-defined).  Only t is produced here;
 // the closest-hit search keeps (t, object) and the hit attributes are
 // computed once for the winner.  The per-lane trip count diverges; the wave
 // leaves the loop when its EXEC mask drains.
-template <class EVAL, bool ANY = false>
+//
+// CONVEX (marches of objects whose SDF program is a convex, 1-Lipschitz function of p: a convex leaf
+// or an intersection of such, no deformers; sdf_convex) adds an exact early miss.  Along
+// the ray, f(t) = sdf(o + t d) is convex, so for t >= t_k it lies above the secant through the last
+// two march points: f(t) >= f(t_k) + s (t - t_k), s = (f(t_k) - f(t_k-1)) / (t_k - t_k-1).  Every
+// computed value d~ is within D of f at the exact point (D = 2^-16 (|o|_1 + tend + |c|_1 + 4 R)
+// absorbs the rounding of p = o + t d, 1-Lipschitz, and of the evaluation, O(2^-24) relative to
+// those magnitudes).  Hence if d~_k - E t_k >= 3D and (d~_k - d~_k-1) - E (t_k - t_k-1) >= 3D with
+// E = eps (1 + 2^-20) >= fl(eps t) / t, every later step has d~ >= f - D >= E t >= fl(eps t): no
+// later step can hit, and the march's answer is "miss" whether it ends at tend or at max_steps.  A
+// NaN anywhere fails both tests.  Shadow rays leaving the object they start on exit after ~3 steps
+// instead of marching out of the bound; camera and shadow rays that pass an object exit once they
+// recede from it.  (A miss's t is never used, so closest-hit marches take it too.)
+template <class EVAL, bool ANY = false, bool CONVEX = false>
 __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
                                           float& t_hit) {
     f3 bc = V(pr.p[0], pr.p[1], pr.p[2]);
@@ -412,6 +458,28 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     // t sequence and result as "if (d < eps*t) hit; t += d*scale; if (t > tend) miss" (NaN
     // included).  (A fully predicated form with a wave-uniform exit was measured slower.)
     bool hit = false;
+    if constexpr (CONVEX) {
+        const float E = eps * (1.0f + 0x1p-20f);
+        const float D3 = 3.0f * 0x1p-16f *
+                         ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
+                          (((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br));
+        float dp = __builtin_nanf(""), tp = t;
+#pragma unroll 1
+        for (uint32_t i = 0; i < steps; ++i) {
+            f3 p = ray_at(r, t);
+            float d = eval(p);
+            hit = d < eps * t;
+            const float tn = t + d * scale;
+            const bool safe = (d - E * t >= D3) && ((d - dp) - E * (t - tp) >= D3);
+            const bool stop = hit || tn > tend || safe;
+            dp = d;
+            tp = t;
+            t = hit ? t : tn;
+            if (stop) break;
+        }
+        t_hit = t;
+        return hit;
+    }
 #pragma unroll 1
     for (uint32_t i = 0; i < steps; ++i) {
         f3 p = ray_at(r, t);
@@ -679,11 +747,11 @@ __device__ __forceinline__ bool isect_capsule(const DPrim& pr, const Ray& r, flo
     return found;
 }
 
-template <bool NEED_HIT, class EVAL, bool ANY = false>
+template <bool NEED_HIT, class EVAL, bool ANY = false, bool CONVEX = false>
 __device__ __forceinline__ bool isect_sdf(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
                                           Hit& out) {
     float t;
-    if (!sdf_march<EVAL, ANY>(pr, eval, r, t_min, t_max, t)) return false;
+    if (!sdf_march<EVAL, ANY, CONVEX>(pr, eval, r, t_min, t_max, t)) return false;
     if (NEED_HIT) sdf_hit_attributes(eval, r, t, out);
     else out.t = t;
     return true;
@@ -860,7 +928,9 @@ __device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, f
     else if constexpr (kind == RRTE_PRIM_CONE) return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_CAPSULE) return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_SDF)
-        return isect_sdf<NEED_HIT, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>, ANY>(
+        return isect_sdf<NEED_HIT, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>, ANY,
+                         (ANY ? kSecantExit >= 1 : kSecantExit >= 2) &&
+                             sdf_convex(S::nodes + pr.sdf_first, pr.sdf_count)>(
             pr, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_MESH) return isect_mesh<ANY>(pr, sc.mesh, r, t_min, t_max, out);
     else return false;

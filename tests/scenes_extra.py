@@ -168,3 +168,35 @@ def nan_left_operand_scene(w, h, mode="lambert_shadow"):
     cfg = RaytracerConfig(max_depth=1, samples_per_pixel=1, width=w, height=h, jitter="center", mode=mode,
                           background_color=Color(0.05, 0.05, 0.08, 1))
     return objs, lights, cam, cfg
+
+
+def convex_sdf_scene(w, h, mode="lambert_shadow"):
+    """Every convex SDF kind the secant early miss applies to (sphere, box, cylinder, prism, cone,
+    capsule, an intersection; degenerate sizes: a negative box extent, an inverted capsule) packed
+    close together with non-convex controls (torus, union, cone with a negative radius), lit by a
+    light near the horizon and one overhead: many grazing shadow rays, and shadow rays that start on
+    one convex object and skim its neighbours (ray_kernels.hpp sdf_march CONVEX)."""
+    from rrte_amd import renderer as R
+
+    ms = [LambertianMaterial(Color.rgb(*c)) for c in [(0.7, 0.5, 0.3), (0.3, 0.6, 0.8), (0.5, 0.8, 0.4)]]
+    y = 1.0
+    sdfs = [R.SDFSphere((-3.0, y, -1.0), 0.9), R.SDFBox((-1.6, y, -1.2), (1.2, 1.6, 1.0)),
+            R.SDFCylinder((-0.2, y, -1.0), 0.6, 1.8), R.SDFPrism((1.2, y, -1.1), (1.2, 1.6, 0.8)),
+            R.SDFCone((2.6, y, -1.0), 0.8, 1.9), R.SDFCapsule((-2.4, y, 0.9), 0.5, 1.2),
+            R.CSGComposite(R.SDFSphere((-0.6, y, 1.0), 0.9), R.SDFBox((-0.3, y, 1.0), (1.2, 1.2, 1.2)),
+                           "intersection"),
+            R.SDFBox((0.9, y, 1.1), (1.0, -0.5, 1.0)), R.SDFCapsule((2.2, y, 1.0), 0.45, -0.6),
+            R.SDFTorus((0.4, 0.4, 2.6), 0.7, 0.25),
+            R.CSGComposite(R.SDFSphere((-2.0, 0.6, 2.6), 0.6), R.SDFSphere((-1.4, 0.6, 2.6), 0.6), "union"),
+            R.SDFCone((2.0, 0.7, 2.6), -0.6, 1.2)]
+    objs = [Sphere((0.0, -1000.0, 0.0), 1000.0, LambertianMaterial(Color.rgb(0.2, 0.2, 0.2)))]
+    objs += [SDFObject(s, ms[i % 3]) for i, s in enumerate(sdfs)]
+    lights = [PointLight((-12.0, 1.3, 0.3), Color.rgb(1.0, 0.9, 0.8), 30.0),
+              PointLight((0.5, 7.0, 0.5), Color.rgb(0.6, 0.7, 1.0), 12.0),
+              DirectionalLight((1.0, -0.05, -0.2), Color.rgb(0.9, 0.9, 1.0), 0.5)]
+    cam = Camera.new_perspective(to_radians(50.0), f32(w) / f32(h), 0.1, 100.0)
+    cam.transform.position = vec3(1.0, 4.5, 8.0)
+    cam.look_at((0.0, 0.8, 0.5))
+    cfg = RaytracerConfig(max_depth=1, samples_per_pixel=1, width=w, height=h, jitter="center", mode=mode,
+                          background_color=Color(0.05, 0.05, 0.08, 1))
+    return objs, lights, cam, cfg

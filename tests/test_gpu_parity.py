@@ -95,7 +95,8 @@ def test_deformation_stress_4k(jit):
     compare(*scenes.deformation_stress(3840, 2160), threads=16, jit=jit)
 
 
-@pytest.mark.parametrize("fn", [se.mixed_scene, se.all_lights_scene, se.deformers_scene, se.ortho_scene])
+@pytest.mark.parametrize("fn", [se.mixed_scene, se.all_lights_scene, se.deformers_scene, se.ortho_scene,
+                                se.convex_sdf_scene])
 @pytest.mark.parametrize("mode", ["refcompat", "lambert_shadow"])
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
 def test_extra_scenes(fn, mode, jit):
@@ -127,6 +128,27 @@ def test_shadow_culling_is_exact(case, jit, monkeypatch):
         out[cull] = (lin.view(np.uint32).copy(), int(rt.stats().shadow_rays))
     assert np.array_equal(out["0"][0], out["1"][0])
     assert out["0"][1] == out["1"][1]
+
+
+@pytest.mark.parametrize("size", [(240, 160), (641, 359)])
+def test_convex_secant_early_miss_is_exact(size, monkeypatch):
+    """Scene-specialised any-hit marches of convex SDF objects stop once the secant bound proves
+    that no later step can hit (ray_kernels.hpp sdf_march CONVEX).  Exact: the image and the
+    shadow-ray count match the oracle bit for bit, and match the same kernel compiled without the
+    early miss (RRTE_JIT_EXTRA_OPTS=-DRRTE_SECANT_EXIT=0), with grazing and near-horizon lights,
+    degenerate convex sizes and non-convex controls."""
+    objs, lights, cam, cfg = se.convex_sdf_scene(*size)
+    compare(objs, lights, cam, cfg, jit=abi.JIT_ON)
+    out = {}
+    for opt in ("", "-DRRTE_SECANT_EXIT=0"):
+        monkeypatch.setenv("RRTE_JIT_EXTRA_OPTS", opt)
+        rt = Raytracer(cfg, device=0, jit=abi.JIT_ON)
+        _, lin = rt.render_f32(objs, lights, [], cam, linear=True)
+        st = rt.stats()
+        assert st.jit_active == 1
+        out[opt] = (lin.view(np.uint32).copy(), int(st.shadow_rays))
+    assert np.array_equal(out[""][0], out["-DRRTE_SECANT_EXIT=0"][0])
+    assert out[""][1] == out["-DRRTE_SECANT_EXIT=0"][1]
 
 
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
