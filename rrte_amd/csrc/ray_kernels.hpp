@@ -340,50 +340,6 @@ struct SdfProgram {
     }
 };
 
-// Static program (scene-specialised kernel): nodes [FIRST, FIRST+COUNT) of a
-// constexpr scene, unrolled at compile time; ops fold, stack slots become
-// fixed registers.  A guarded operand [I, J) becomes a uniform branch around
-// its straight-line code.
-template <class S, uint32_t FIRST, uint32_t I, uint32_t END, bool CHECK>
-__device__ __forceinline__ void sdf_static_range(float* vs, f3* ps, uint32_t& sp, uint32_t& pp, f3& p) {
-    if constexpr (I < END) {
-        constexpr rrte_sdf_node n = S::nodes[FIRST + I];
-        constexpr uint32_t link = n.i[2];
-        if constexpr (CHECK && link != 0u) {
-            constexpr rrte_sdf_node g = S::nodes[FIRST + link - 1u];
-            float r;
-            if (sdf_guard(g, vs[sp - 1], p, r)) vs[sp - 1] = r;
-            else sdf_static_range<S, FIRST, I, link, false>(vs, ps, sp, pp, p);
-            sdf_static_range<S, FIRST, link, END, true>(vs, ps, sp, pp, p);
-        } else {
-            sdf_node_step(n, vs, ps, sp, pp, p);
-            sdf_static_range<S, FIRST, I + 1u, END, true>(vs, ps, sp, pp, p);
-        }
-    }
-}
-
-template <class S, uint32_t FIRST, uint32_t COUNT>
-struct SdfStaticProgram {
-    __device__ __forceinline__ float operator()(f3 p) const {
-        float vs[RRTE_SDF_MAX_STACK];
-        f3 ps[RRTE_SDF_MAX_POINT_STACK];
-        uint32_t sp = 0, pp = 0;
-        sdf_static_range<S, FIRST, 0u, COUNT, true>(vs, ps, sp, pp, p);
-        return vs[0];
-    }
-};
-
-// Exact "ray leaves the sphere" early-out for any-hit (shadow) rays: origin outside the sphere
-// (cc = |oc|^2 - r^2 > 0) moving away from its centre (hb = oc.d > 0), |d|^2 >= 1/4, t_min >= 2^-57.
-// Then the full test finds nothing in [t_min, t_max]: disc = RN(RN(hb^2) - RN(a cc)) <= RN(hb^2), so
-// sq = RN(sqrt(disc)) <= RN(sqrt(RN(hb^2))), which is hb when hb >= 2^-60 (fl(sqrt(fl(x*x))) = |x| in
-// binary f32 with round-to-nearest, no under/overflow) and <= 2^-60 otherwise; hence -hb + sq <= 2^-60,
-// both roots (-hb -/+ sq)/a are <= 2^-58 < t_min, and the sphere / bounding-sphere test rejects.
-// Skips the sqrt and divides of, e.g., every shadow ray's test against the ground sphere.
-__device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float t_min) {
-    return hb > 0.0f && cc > 0.0f && a >= 0.25f && t_min >= 0x1p-57f;
-}
-
 // Is the postfix program a convex, 1-Lipschitz function of p?  Convex leaves (exact SDFs of convex
 // solids -- the signed distance of a convex set is a supremum of affine functions -- and the prism's
 // max of 1-Lipschitz convex terms) and intersections (max) of such; union, difference, smooth ops,
@@ -416,6 +372,63 @@ constexpr bool sdf_convex(const rrte_sdf_node* n, uint32_t count) {
     }
     return sp == 1u && st[0];
 }
+// Scale of a program's leaves for sdf_march's error bound: max over leaves of |center|_1 + the sum
+// of |size parameters| (an intersection's leaves may reach far outside the object's bound).
+constexpr float sdf_leaf_scale(const rrte_sdf_node* n, uint32_t count) {
+    float k = 0.0f;
+    for (uint32_t i = 0; i < count; ++i) {
+        if (n[i].op >= 32u) continue;
+        float s = 0.0f;
+        for (int j = 0; j < 7; ++j) s += n[i].f[j] < 0.0f ? -n[i].f[j] : n[i].f[j];
+        k = s > k ? s : k;
+    }
+    return k;
+}
+
+// Static program (scene-specialised kernel): nodes [FIRST, FIRST+COUNT) of a
+// constexpr scene, unrolled at compile time; ops fold, stack slots become
+// fixed registers.  A guarded operand [I, J) becomes a uniform branch around
+// its straight-line code.
+template <class S, uint32_t FIRST, uint32_t I, uint32_t END, bool CHECK>
+__device__ __forceinline__ void sdf_static_range(float* vs, f3* ps, uint32_t& sp, uint32_t& pp, f3& p) {
+    if constexpr (I < END) {
+        constexpr rrte_sdf_node n = S::nodes[FIRST + I];
+        constexpr uint32_t link = n.i[2];
+        if constexpr (CHECK && link != 0u) {
+            constexpr rrte_sdf_node g = S::nodes[FIRST + link - 1u];
+            float r;
+            if (sdf_guard(g, vs[sp - 1], p, r)) vs[sp - 1] = r;
+            else sdf_static_range<S, FIRST, I, link, false>(vs, ps, sp, pp, p);
+            sdf_static_range<S, FIRST, link, END, true>(vs, ps, sp, pp, p);
+        } else {
+            sdf_node_step(n, vs, ps, sp, pp, p);
+            sdf_static_range<S, FIRST, I + 1u, END, true>(vs, ps, sp, pp, p);
+        }
+    }
+}
+
+template <class S, uint32_t FIRST, uint32_t COUNT>
+struct SdfStaticProgram {
+    static constexpr float kLeafScale = sdf_leaf_scale(S::nodes + FIRST, COUNT);
+    __device__ __forceinline__ float operator()(f3 p) const {
+        float vs[RRTE_SDF_MAX_STACK];
+        f3 ps[RRTE_SDF_MAX_POINT_STACK];
+        uint32_t sp = 0, pp = 0;
+        sdf_static_range<S, FIRST, 0u, COUNT, true>(vs, ps, sp, pp, p);
+        return vs[0];
+    }
+};
+
+// Exact "ray leaves the sphere" early-out for any-hit (shadow) rays: origin outside the sphere
+// (cc = |oc|^2 - r^2 > 0) moving away from its centre (hb = oc.d > 0), |d|^2 >= 1/4, t_min >= 2^-57.
+// Then the full test finds nothing in [t_min, t_max]: disc = RN(RN(hb^2) - RN(a cc)) <= RN(hb^2), so
+// sq = RN(sqrt(disc)) <= RN(sqrt(RN(hb^2))), which is hb when hb >= 2^-60 (fl(sqrt(fl(x*x))) = |x| in
+// binary f32 with round-to-nearest, no under/overflow) and <= 2^-60 otherwise; hence -hb + sq <= 2^-60,
+// both roots (-hb -/+ sq)/a are <= 2^-58 < t_min, and the sphere / bounding-sphere test rejects.
+// Skips the sqrt and divides of, e.g., every shadow ray's test against the ground sphere.
+__device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float t_min) {
+    return hb > 0.0f && cc > 0.0f && a >= 0.25f && t_min >= 0x1p-57f;
+}
 
 // SDFObject::intersect, search part -- sphere tracing inside the object's
 // bounding sphere (build-defined).  Only t is produced here;
@@ -427,9 +440,12 @@ constexpr bool sdf_convex(const rrte_sdf_node* n, uint32_t count) {
 // or an intersection of such, no deformers; sdf_convex) adds an exact early miss.  Along
 // the ray, f(t) = sdf(o + t d) is convex, so for t >= t_k it lies above the secant through the last
 // two march points: f(t) >= f(t_k) + s (t - t_k), s = (f(t_k) - f(t_k-1)) / (t_k - t_k-1).  Every
-// computed value d~ is within D of f at the exact point (D = 2^-16 (|o|_1 + tend + |c|_1 + 4 R)
-// absorbs the rounding of p = o + t d, 1-Lipschitz, and of the evaluation, O(2^-24) relative to
-// those magnitudes).  Hence if d~_k - E t_k >= 3D and (d~_k - d~_k-1) - E (t_k - t_k-1) >= 3D with
+// computed value d~ is within D of f at the exact point: D = 2^-17 (|o|_1 + tend + |c|_1 + 4 R + K),
+// K = sdf_leaf_scale (the largest leaf's |center|_1 + |sizes|).  The rounding of p = o + t d moves
+// p by <= 2^-24 (|o|_1 + 2t), which f (1-Lipschitz) passes on unchanged, and each leaf's evaluation
+// errs by <= 24 * 2^-24 (|q| + sizes), the cone's being the longest (its clamped projection
+// parameter's error times the side length stays <= 8 * 2^-24 (|q| + h)); together <= 50 * 2^-24
+// (...) against 2^-17 = 128 * 2^-24.  Hence if d~_k - E t_k >= 3D and (d~_k - d~_k-1) - E (t_k - t_k-1) >= 3D with
 // E = eps (1 + 2^-20) >= fl(eps t) / t, every later step has d~ >= f - D >= E t >= fl(eps t): no
 // later step can hit, and the march's answer is "miss" whether it ends at tend or at max_steps.  A
 // NaN anywhere fails both tests.  Shadow rays leaving the object they start on exit after ~3 steps
@@ -460,9 +476,10 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     bool hit = false;
     if constexpr (CONVEX) {
         const float E = eps * (1.0f + 0x1p-20f);
-        const float D3 = 3.0f * 0x1p-16f *
+        constexpr float K = EVAL::kLeafScale;
+        const float D3 = 3.0f * 0x1p-17f *
                          ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
-                          (((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br));
+                          ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
         float dp = __builtin_nanf(""), tp = t;
 #pragma unroll 1
         for (uint32_t i = 0; i < steps; ++i) {
