@@ -363,7 +363,10 @@ constexpr bool sdf_convex(const rrte_sdf_node* n, uint32_t count) {
                        (op == RRTE_SDF_CONE && n[i].f[3] > 0.0f && n[i].f[4] > 0.0f);
         } else if (op < 64u) {
             if (sp < 2u) return false;
-            const bool c = op == RRTE_SDF_INTERSECTION && st[sp - 1] && st[sp - 2];
+            // max, and the smooth max -smin(-a, -b, k) = (a + b)/2 + phi(a - b) with phi(u) = k/4 + u^2/(4k)
+            // for |u| <= k, |u|/2 beyond (convex, nondecreasing in a and b, 1-Lipschitz), k > 0
+            const bool c = (op == RRTE_SDF_INTERSECTION || (op == RRTE_SDF_SMOOTH_INTERSECTION && n[i].f[0] > 0.0f)) &&
+                           st[sp - 1] && st[sp - 2];
             sp -= 2;
             st[sp++] = c;
         } else {
@@ -373,16 +376,20 @@ constexpr bool sdf_convex(const rrte_sdf_node* n, uint32_t count) {
     return sp == 1u && st[0];
 }
 // Scale of a program's leaves for sdf_march's error bound: max over leaves of |center|_1 + the sum
-// of |size parameters| (an intersection's leaves may reach far outside the object's bound).
+// of |size parameters| (an intersection's leaves may reach far outside the object's bound), plus
+// every smooth op's |k|.
 constexpr float sdf_leaf_scale(const rrte_sdf_node* n, uint32_t count) {
-    float k = 0.0f;
+    float k = 0.0f, ks = 0.0f;
     for (uint32_t i = 0; i < count; ++i) {
-        if (n[i].op >= 32u) continue;
+        if (n[i].op >= 32u) {
+            if (n[i].op < 64u) ks += n[i].f[0] < 0.0f ? -n[i].f[0] : n[i].f[0];
+            continue;
+        }
         float s = 0.0f;
         for (int j = 0; j < 7; ++j) s += n[i].f[j] < 0.0f ? -n[i].f[j] : n[i].f[j];
         k = s > k ? s : k;
     }
-    return k;
+    return k + ks;
 }
 
 // Static program (scene-specialised kernel): nodes [FIRST, FIRST+COUNT) of a
@@ -444,7 +451,8 @@ __device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float
 // K = sdf_leaf_scale (the largest leaf's |center|_1 + |sizes|).  The rounding of p = o + t d moves
 // p by <= 2^-24 (|o|_1 + 2t), which f (1-Lipschitz) passes on unchanged, and each leaf's evaluation
 // errs by <= 24 * 2^-24 (|q| + sizes), the cone's being the longest (its clamped projection
-// parameter's error times the side length stays <= 8 * 2^-24 (|q| + h)); together <= 50 * 2^-24
+// parameter's error times the side length stays <= 8 * 2^-24 (|q| + h)), a smooth max adds
+// <= 6 * 2^-24 (|a| + |b| + k) and passes its operands' errors on unscaled; together <= 64 * 2^-24
 // (...) against 2^-17 = 128 * 2^-24.  Hence if d~_k - E t_k >= 3D and (d~_k - d~_k-1) - E (t_k - t_k-1) >= 3D with
 // E = eps (1 + 2^-20) >= fl(eps t) / t, every later step has d~ >= f - D >= E t >= fl(eps t): no
 // later step can hit, and the march's answer is "miss" whether it ends at tend or at max_steps.  A

@@ -172,7 +172,7 @@ def nan_left_operand_scene(w, h, mode="lambert_shadow"):
 
 def convex_sdf_scene(w, h, mode="lambert_shadow"):
     """Every convex SDF kind the secant early miss applies to (sphere, box, cylinder, prism, cone,
-    capsule, an intersection; degenerate sizes: a negative box extent, an inverted capsule) packed
+    capsule, intersections and smooth intersections; degenerate sizes: a negative box extent, an inverted capsule) packed
     close together with non-convex controls (torus, union, cone with a negative radius), lit by a
     light near the horizon and one overhead: many grazing shadow rays, and shadow rays that start on
     one convex object and skim its neighbours (ray_kernels.hpp sdf_march CONVEX)."""
@@ -186,6 +186,10 @@ def convex_sdf_scene(w, h, mode="lambert_shadow"):
             R.CSGComposite(R.SDFSphere((-0.6, y, 1.0), 0.9), R.SDFBox((-0.3, y, 1.0), (1.2, 1.2, 1.2)),
                            "intersection"),
             R.SDFBox((0.9, y, 1.1), (1.0, -0.5, 1.0)), R.SDFCapsule((2.2, y, 1.0), 0.45, -0.6),
+            R.CSGComposite(R.SDFSphere((3.4, y, 0.2), 0.8), R.SDFCylinder((3.7, y, 0.2), 0.6, 1.6),
+                           "smooth_intersection", 0.3),
+            R.CSGComposite(R.SDFCone((-3.6, 0.8, 2.2), 0.7, 1.6), R.SDFSphere((-3.5, 0.8, 2.2), 0.7),
+                           "smooth_intersection", 0.05),
             R.SDFTorus((0.4, 0.4, 2.6), 0.7, 0.25),
             R.CSGComposite(R.SDFSphere((-2.0, 0.6, 2.6), 0.6), R.SDFSphere((-1.4, 0.6, 2.6), 0.6), "union"),
             R.SDFCone((2.0, 0.7, 2.6), -0.6, 1.2)]
