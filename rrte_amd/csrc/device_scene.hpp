@@ -68,7 +68,7 @@ struct FrameCam {
     // Camera-ray tile culling (perspective frames, objects [0, tile_n), tile_n <= 32): object i's
     // bounding sphere projects inside the tile rectangle tile_rect[i] = bx0 | bx1 << 8 | by0 << 16 |
     // by1 << 24 (inclusive, conservative; tiles of 1 << tile_cull pixels: 3 = 8x8 per wave,
-    // 4 = 16x16 per workgroup); a tile outside it cannot hit object i with a camera ray.  0: off.
+    // 4 = 16x16, four 8x8 workgroups); a tile outside it cannot hit object i with a camera ray.  0: off.
     uint32_t tile_cull, tile_n;
     uint32_t tile_rect[32];
 };

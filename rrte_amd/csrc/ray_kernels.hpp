@@ -2,7 +2,7 @@
 //
 // One wave64 lane per pixel, one wave per 8x8 pixel tile (rays in a wave are
 // spatially coherent, so the wave-uniform object loop and the sphere-tracing
-// loop diverge little), 4 waves per 256-thread workgroup.  Scene records are
+// loop diverge little), one wave per 64-thread workgroup.  Scene records are
 // read with wave-uniform indices -> scalar loads into SGPRs; no MFMA (there is
 // no dense contraction on this path).  Operation order mirrors the reference
 // (file:line cited per function, paths relative to Melthizar/RRTE).
@@ -820,9 +820,21 @@ __device__ __forceinline__ bool mesh_tri_hit(const MeshView& mv, uint32_t k, con
     return true;
 }
 
+// Workgroup geometry: one wave per workgroup, one 8x8 pixel tile each (kBlockThreads = 64).  A
+// workgroup's waves must start together on one CU and a 4-wave workgroup needs a free slot on every
+// SIMD, so with a few long-running (grazing-ray) waves resident, 256-thread workgroups of 16x16 pixels
+// left slots idle that single waves fill: -9 % per frame.  RRTE_WG256 (defined by the
+// host for RRTE_WG64=0, an A/B switch for the specialised kernels) restores the 256-thread layout.
+#ifdef RRTE_WG256
+constexpr bool kWg64 = false;
+#else
+constexpr bool kWg64 = true;
+#endif
+constexpr uint32_t kBlockThreads = kWg64 ? 64u : 256u;
+
 constexpr int kMeshStack = 32;  // BVH depth is capped below this at build time
 __device__ __forceinline__ uint32_t* mesh_stack() {
-    __shared__ uint32_t stk[kMeshStack * 256];  // [depth][lane of the 256-thread workgroup]
+    __shared__ uint32_t stk[kMeshStack * kBlockThreads];  // [depth][lane of the workgroup]
     return stk + threadIdx.x;
 }
 
@@ -878,7 +890,7 @@ __device__ __forceinline__ bool isect_mesh(const DPrim& pr, const MeshView& mv, 
                 const uint32_t c0 = __float_as_uint(l0.w), c1 = __float_as_uint(l1.w);
                 if (t0 != kInf && t1 != kInf) {
                     const bool near0 = t0 <= t1;
-                    stk[(sp++) * 256] = near0 ? c1 : c0;
+                    stk[(sp++) * kBlockThreads] = near0 ? c1 : c0;
                     link = near0 ? c0 : c1;
                     continue;
                 }
@@ -909,7 +921,7 @@ __device__ __forceinline__ bool isect_mesh(const DPrim& pr, const MeshView& mv, 
                 if (ANY && found) break;
             }
             if (sp == 0) break;
-            link = stk[(--sp) * 256];
+            link = stk[(--sp) * kBlockThreads];
         }
     }
     out.t = best;
@@ -1608,7 +1620,7 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
     return (b * kp.nranks + kp.rank) * kp.band_rows + w;
 }
 
-// Camera-ray tile culling mask of this wave's 8x8 tile (kp.tile_cull = 3) or its workgroup's 16x16
+// Camera-ray tile culling mask of this wave's 8x8 tile (kp.tile_cull = 3) or the 16x16
 // block (4) (KParams::tile_rect): lane j tests object j's rectangle and a ballot makes the mask
 // wave-uniform (one load and a handful of VALU ops per wave; a scalar loop over the objects cost ~8
 // SALU ops and a scalar load each).  Call with all 64 lanes active.  The host enables it only when
@@ -1617,9 +1629,15 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
 __device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp, const FrameCam& cm) {
     const uint32_t sh = cm.tile_cull;
     if (!sh) return ~0u;
-    const uint32_t wave = sh == 3u ? (threadIdx.x >> 6) : 0u;
-    const uint32_t bx = (blockIdx.x * 16u + (wave & 1u) * 8u) >> sh;
-    const uint32_t by = image_row(kp, blockIdx.y * 16u + (wave >> 1) * 8u) >> sh;
+    uint32_t bx, by;
+    if (kWg64) {  // one 8x8 tile per workgroup
+        bx = (blockIdx.x * 8u) >> sh;
+        by = image_row(kp, blockIdx.y * 8u) >> sh;
+    } else {
+        const uint32_t wave = sh == 3u ? (threadIdx.x >> 6) : 0u;
+        bx = (blockIdx.x * 16u + (wave & 1u) * 8u) >> sh;
+        by = image_row(kp, blockIdx.y * 16u + (wave >> 1) * 8u) >> sh;
+    }
     const uint32_t j = threadIdx.x & 63u;
     bool in = false;
     if (j < cm.tile_n) {
@@ -1630,7 +1648,7 @@ __device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp, const Fr
     return m | (cm.tile_n < 32u ? (~0u << cm.tile_n) : 0u);  // objects past the table: never culled
 }
 
-// One lane per pixel; wave = 8x8 tile, workgroup = 16x16 pixels.  Every lane
+// One lane per pixel; wave = workgroup = 8x8 tile (RRTE_WG256: 16x16-pixel workgroups).  Every lane
 // of a wave runs the sample loop (lanes past the image edge are idle but
 // present) so the culling reductions see converged waves.  CULL selects the
 // shadow-culled LAMBERT_SHADOW variant (the host picks it per scene).
@@ -1638,7 +1656,7 @@ template <int MODE, class S, bool SINGLE = false, bool CULL = false>
 __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, const Cull& cl,
                                                 uint32_t* __restrict__ out_rgba8, float4* __restrict__ out_f32,
                                                 unsigned long long* __restrict__ counters) {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u, wave = kWg64 ? 0u : threadIdx.x >> 6;
     // frame blockIdx.z of the launch: its camera, its output (multi-frame launches have no f32 output)
     const FrameCam& cm = kp.cam[blockIdx.z];
     if (out_rgba8 && blockIdx.z)
@@ -1650,8 +1668,8 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     const uint32_t brow = blockIdx.y;
     if ((kp.debug & 32u) && brow * gridDim.x + blockIdx.x != (kp.debug >> 16)) return;
     const uint64_t t_wave0 = stamps ? wall_clock64() : 0ull;
-    const uint32_t x = blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t lr = brow * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const uint32_t x = kWg64 ? blockIdx.x * 8u + (lane & 7u) : blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t lr = kWg64 ? brow * 8u + (lane >> 3) : brow * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool live = x < kp.width && lr < kp.rows;
     const uint32_t xc = live ? x : 0u;
     const uint32_t y = image_row(kp, live ? lr : 0u);
@@ -1781,7 +1799,7 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
 
 // Generic kernel: the scene is read from HBM through wave-uniform (scalar) loads.
 template <int MODE, bool CULL>
-__global__ __launch_bounds__(256) void ray_kernel(KParams kp, SceneView sc, Cull cl, uint32_t* __restrict__ out_rgba8,
+__global__ __launch_bounds__(kBlockThreads) void ray_kernel(KParams kp, SceneView sc, Cull cl, uint32_t* __restrict__ out_rgba8,
                                                   float4* __restrict__ out_f32,
                                                   unsigned long long* __restrict__ counters) {
     ray_kernel_body<MODE, SceneView, false, CULL>(kp, sc, cl, out_rgba8, out_f32, counters);

@@ -123,6 +123,7 @@ struct rrte_ctx {
     bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
     bool env_gather_rgba = false;   // RRTE_GATHER_RGB24=0: gather slabs always RGBA8
     uint32_t env_guard_leaves = 2;  // RRTE_CSG_GUARDS: 0 = off, N = smallest guarded operand (leaves)
+    bool env_wg256 = false;           // RRTE_WG64=0: specialised kernels in 256-thread workgroups (A/B only)
     int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, valid; JitKernel* k; } jit_last{};
@@ -616,7 +617,7 @@ void fill_tile_rects(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_rende
     const uint32_t band_rows = kk.band_rows;
     k.tile_cull = 0;
     // 8x8 tiles (one per wave) when their indices fit 8 bits and bands keep 8-row tiles whole,
-    // else 16x16 blocks (one per workgroup)
+    // else 16x16 blocks (four 8x8 workgroups)
     auto fits = [&](uint32_t sh) {
         const uint32_t t = 1u << sh;
         return (p->width + t - 1) / t <= 256 && (p->height + t - 1) / t <= 256 &&
@@ -773,6 +774,7 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
         std::string src = jit_source(c->h_prims.data(), (uint32_t)c->h_prims.size(), c->h_mats.data(),
                                      (uint32_t)c->h_mats.size(), c->h_lights.data(), (uint32_t)c->h_lights.size(),
                                      c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull, single);
+        if (c->env_wg256) src = "#define RRTE_WG256 1\n" + src;
         if (c->jit_mode == RRTE_JIT_AUTO) {
             // compile on a background thread (hiprtc only); frames keep running on the generic kernel
             c->jit_pending.emplace(key, std::async(std::launch::async, [src]() { return jit_compile_code(src); }));
@@ -803,8 +805,8 @@ LaunchPlan plan_launch(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_ren
     L.num_prims = s->num_prims;
     L.num_lights = s->num_lights;
     L.num_materials = s->num_materials;
-    L.gx = (p->width + 15) / 16;
-    L.gy = (rows + 15) / 16;
+    L.gx = (p->width + 7) / 8;  // one 8x8 tile per 64-thread workgroup (kBlockThreads)
+    L.gy = (rows + 7) / 8;
     fill_tile_rects(c, s, p, L.k);
     return L;
 }
@@ -813,7 +815,7 @@ LaunchPlan plan_launch(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_ren
 rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     if (L.gy == 0) return RRTE_OK;
     Cull cl{L.cull ? c->d_bounds : nullptr, L.num_prims};
-    const dim3 grid(L.gx, L.gy, L.k.nframes), block(256);
+    const dim3 grid(L.gx, L.gy, L.k.nframes), block(kBlockThreads);
     JitKernel* jk = jit_kernel_for(c, L.mode, L.cull, L.single);
     c->stats.jit_active = jk ? 1u : 0u;
     if (jk) {
@@ -821,7 +823,11 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         MeshView mv = c->mesh_view;
         void* args[] = {&L.k, &cl, &mv, &d_rgba, &d_f32, &ctr};
         HostSection hs(c);
-        HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, 256, 1, 1, 0, st, args, nullptr));
+        if (c->env_wg256)
+            HIPCHK(c, hipModuleLaunchKernel(jk->fn, (L.k.width + 15) / 16, (L.k.rows + 15) / 16, grid.z, 256, 1, 1, 0,
+                                            st, args, nullptr));
+        else
+            HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, st, args, nullptr));
         hs.lap(8);
         return RRTE_OK;
     }
@@ -951,6 +957,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_DIAG_SKIP")) c->env_diag_skip = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GATHER_RGB24")) c->env_gather_rgba = g[0] == '0';
     c->env_guard_leaves = env_guard_setting();
+    if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
         if (sscanf(e, "%d:%d", &n, &r) == 2 && n > 1 && r >= 0 && r < n) {
