@@ -1714,6 +1714,8 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
                     active = true;
                 }
                 if (!__any(active)) break;
+                // (camera-ray tile culling while every active lane is on its camera ray was measured
+                // slower, 0.94 -> 1.00 ms on the stock config: the runtime mask costs every bounce)
                 if (active && path_step(sc, kp, ps, st)) {
                     accumulate(ps.out);
                     active = false;

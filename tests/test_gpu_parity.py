@@ -267,6 +267,28 @@ def test_camera_tile_culling_is_exact(name, jit, monkeypatch):
 
 
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+@pytest.mark.parametrize("name", ["sdf-showcase", "advanced-demo"])
+def test_camera_tile_culling_in_the_path_loop_is_exact(name, jit, monkeypatch):
+    """REFCOMPAT with spp > 1 and depth > 1 (the path-regeneration loop): the tile mask applies while
+    every active lane of a wave is on its camera ray; culling on and off give identical images."""
+    rts = {}
+    for tc in ("0", "1"):
+        monkeypatch.setenv("RRTE_TILE_CULL", tc)
+        rts[tc] = Raytracer(scenes.SCENES[name](64, 36, mode="refcompat")[3], device=0, jit=jit)
+    for w, h in ((131, 77), (2101, 40)):
+        for pos, tgt, fov in [((0.0, 8.0, 20.0), (0.0, 2.0, 0.0), 45.0), ((3.0, 1.0, 3.0), (12.0, 2.0, 0.0), 100.0)]:
+            objs, lights, _, cfg = scenes.SCENES[name](w, h, mode="refcompat")
+            cfg.samples_per_pixel, cfg.max_depth, cfg.jitter = 3, 6, "random"
+            cam = scenes._camera(w, h, pos, tgt, fov)
+            out = {}
+            for tc, rt in rts.items():
+                rt.update_config(cfg)
+                _, lin = rt.render_f32(objs, lights, [], cam, linear=True)
+                out[tc] = lin.view(np.uint32).copy()
+            assert np.array_equal(out["0"], out["1"]), (name, w, h, pos)
+
+
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
 @pytest.mark.parametrize("band", [8, 16])
 def test_camera_tile_culling_with_band_mapping(band, jit, monkeypatch):
     """Tile culling on one rank's share of a multi-GPU frame (KParams::band_rows > 0: local rows map
