@@ -191,9 +191,26 @@ __device__ __forceinline__ float smn(float a, float b) { return __builtin_fminf(
 __device__ __forceinline__ float smx(float a, float b) { return __builtin_fmaxf(a, b); }
 __device__ __forceinline__ float sclamp(float x, float lo, float hi) { return smn(smx(x, lo), hi); }
 
+// vnorm for a vector already normalised once (|w|^2 within a few ulp of 1: a light direction, a
+// rotated unit camera direction), bit-identical to vnorm: with x = fl(w.w) and k = bits(x) -
+// bits(1.0f), RN(1 / RN(sqrt(x))) has the bits 0x3F800000 - (k >= 0 ? k & ~1 : k >> 2) for every
+// |k| <= 1024 (sqrt(1 + d) = 1 + d/2 - d^2/8: RN keeps 1 + floor(k/2) ulp above 1 or rounds half an ulp
+// below 1 away from it, and the reciprocal folds back the same way; checked exhaustively,
+// tests/test_fpexact_cpu.py, first failure at |k| = 2898).  Five integer ops replace the sqrt and
+// reciprocal sequences (12 VALU ops, two guards); other x take vnorm in a divergent branch.
+__device__ __forceinline__ f3 vnorm_unit(f3 w) {
+    const float x = vdot(w, w);
+    const int k = (int)__float_as_uint(x) - 0x3F800000;
+    float r = __int_as_float(0x3F800000 - (k >= 0 ? (k & ~1) : (k >> 2)));
+    if (__builtin_expect((uint32_t)(k + 1024) > 2048u, 0)) r = rcp_rn(sqrt_rn(x));
+    return vmuls(w, r);
+}
+
 struct Ray { f3 o, d; };
 // Ray::new normalises (ray.rs:13-18); Ray::at (ray.rs:21-23)
 __device__ __forceinline__ Ray ray_new(f3 o, f3 d) { return Ray{o, vnorm(d)}; }
+// Ray::new for a direction already of unit length up to rounding (vnorm_unit)
+__device__ __forceinline__ Ray ray_new_unit(f3 o, f3 d) { return Ray{o, vnorm_unit(d)}; }
 __device__ __forceinline__ f3 ray_at(const Ray& r, float t) { return vadd(r.o, vmuls(r.d, t)); }
 
 __device__ __forceinline__ bool finite3(f3 a) {

@@ -1387,13 +1387,13 @@ __device__ __forceinline__ Ray generate_ray(const FrameCam& cm, float u, float v
         float half_w = cm.aspect * cm.half_h;
         f3 cd = vnorm(V(ndc_x * half_w, ndc_y * cm.half_h, -1.0f));
         f3 wd = quat_rotate(cm.cam_rot, cd);
-        return ray_new(V(cm.cam_pos[0], cm.cam_pos[1], cm.cam_pos[2]), wd);
+        return ray_new_unit(V(cm.cam_pos[0], cm.cam_pos[1], cm.cam_pos[2]), wd);
     }
     float wx = cm.ortho_l + (cm.ortho_r - cm.ortho_l) * u;
     float wy = cm.ortho_b + (cm.ortho_t - cm.ortho_b) * v;
     f3 o = m_point(cm.cam_xf, V(wx, wy, 0.0f));
     f3 wd = quat_rotate(cm.cam_rot, V(0.0f, 0.0f, -1.0f));
-    return ray_new(o, wd);
+    return ray_new_unit(o, wd);
 }
 
 // Raytracer::ray_color (raytracer.rs:92-148) for one camera sample.
@@ -1540,7 +1540,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
         const float ndl = vdot(h.n, k.dir);
         if (ndl > 0.0f && k.att > 0.0f) {
             ++nshadow;
-            Ray sr = ray_new(vadd(h.p, vmuls(h.n, bias)), k.dir);
+            Ray sr = ray_new_unit(vadd(h.p, vmuls(h.n, bias)), k.dir);
             // RRTE_DEBUG bit 6 (timing diagnostics only, wrong images): skip the object the ray starts on
             if ((kp.debug & 1u) || !occluded(sc, sr, bias, k.dist, smask, (kp.debug & 64u) ? idx : -1)) {
                 float f = k.att * ndl;
