@@ -128,7 +128,9 @@ __device__ __forceinline__ float sqrt_rn(float x) {
     const float e = __builtin_fmaf(-s, s, x);
     float r = __builtin_fmaf(e, 0.5f * y, s);
     constexpr uint32_t kLo = 0x0F800000u, kInf = 0x7F800000u;  // bits of 2^-96 and +inf
+#ifndef RRTE_ABLATE_NO_GUARDS  // timing experiment only: drops the out-of-range fallback branches
     if (__builtin_expect(__float_as_uint(x) - kLo >= kInf - kLo, 0)) r = __builtin_sqrtf(x);
+#endif
     return r;
 }
 #endif
@@ -139,7 +141,9 @@ __device__ __forceinline__ float rcp_rn(float b) {
     if (__builtin_constant_p(b)) return 1.0f / b;
     float y = __builtin_amdgcn_rcpf(b);
     y = __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
+#ifndef RRTE_ABLATE_NO_GUARDS
     if (__builtin_expect(!(__builtin_fabsf(b) >= 0x1.0p-126f && __builtin_fabsf(b) <= 0x1.0p+126f), 0)) y = 1.0f / b;
+#endif
     return y;
 }
 // Correctly rounded a/b.  When b folds to a constant (scene-specialised kernels: SDF and
@@ -156,7 +160,9 @@ __device__ __forceinline__ float div_by_rcp(float a, float b, float y) {  // y =
 __device__ __forceinline__ float div_rn(float a, float b) {
     if (__builtin_constant_p(b) && __builtin_fabsf(b) >= 0x1.0p-60f && __builtin_fabsf(b) <= 0x1.0p+60f) {
         float r = div_by_rcp(a, b, 1.0f / b);
+#ifndef RRTE_ABLATE_NO_GUARDS
         if (__builtin_expect(!(__builtin_fabsf(a) >= 0x1.0p-60f && __builtin_fabsf(a) <= 0x1.0p+60f), 0)) r = a / b;
+#endif
         return r;
     }
     return a / b;
@@ -202,7 +208,9 @@ __device__ __forceinline__ f3 vnorm_unit(f3 w) {
     const float x = vdot(w, w);
     const int k = (int)__float_as_uint(x) - 0x3F800000;
     float r = __int_as_float(0x3F800000 - (k >= 0 ? (k & ~1) : (k >> 2)));
+#ifndef RRTE_ABLATE_NO_GUARDS
     if (__builtin_expect((uint32_t)(k + 1024) > 2048u, 0)) r = rcp_rn(sqrt_rn(x));
+#endif
     return vmuls(w, r);
 }
 
