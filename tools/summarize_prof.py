@@ -1,6 +1,8 @@
 """Summarize a tools/prof_gpu.sh output dir into profiles/<name>.md and profiles/pmc_<name>.json.
 
 usage: python tools/summarize_prof.py gpurun_out/prof_<tag> <name> <workload-key>
+<workload-key> must be bench.py's key (e.g. sdf-showcase@1920x1080/lambert_shadow): bench.py takes the
+newest summary with that key for the bench line's `roofline.traffic` and `valu` objects.
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) under-reports wide coalesced reads
 by 2x on gfx950 (doubled here, flagged as uncalibrated for this access pattern); WRITE_SIZE (KiB)
 is exact for wide stores; both are per dispatch.
