@@ -461,6 +461,13 @@ __device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float
 // NaN anywhere fails both tests.  Shadow rays leaving the object they start on exit after ~3 steps
 // instead of marching out of the bound; camera and shadow rays that pass an object exit once they
 // recede from it.  (A miss's t is never used, so closest-hit marches take it too.)
+// Unroll factor of the sphere-tracing loops (RRTE_MARCH_UNROLL, A/B experiments through
+// RRTE_JIT_EXTRA_OPTS; the per-lane exit keeps every unrolled copy exact).
+#ifndef RRTE_MARCH_UNROLL
+#define RRTE_MARCH_UNROLL 1
+#endif
+#define RRTE_PRAGMA_(x) _Pragma(#x)
+#define RRTE_UNROLL_(n) RRTE_PRAGMA_(unroll n)
 template <class EVAL, bool ANY = false, bool CONVEX = false>
 __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
                                           float& t_hit) {
@@ -491,7 +498,7 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
                          ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
                           ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
         float dp = __builtin_nanf(""), tp = t;
-#pragma unroll 1
+RRTE_UNROLL_(RRTE_MARCH_UNROLL)
         for (uint32_t i = 0; i < steps; ++i) {
             f3 p = ray_at(r, t);
             float d = eval(p);
@@ -507,7 +514,7 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
         t_hit = t;
         return hit;
     }
-#pragma unroll 1
+RRTE_UNROLL_(RRTE_MARCH_UNROLL)
     for (uint32_t i = 0; i < steps; ++i) {
         f3 p = ray_at(r, t);
         float d = eval(p);
