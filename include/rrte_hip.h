@@ -213,8 +213,8 @@ typedef enum rrte_jitter {
 
 #define RRTE_FLAG_F32_LINEAR 1u  /* f32 output holds the averaged linear colour (pre-gamma, unclamped) */
 /* Accepted and ignored (ABI v2 compatibility).  It used to move each frame's gather onto a comm
- * stream; frames now overlap on the caller's streams through the gather lanes of
- * rrte_hip_comm_init (one communicator per lane), which measured faster. */
+ * stream; frames now overlap through per-frame gathers on the caller's own streams, or through
+ * batched gathers (rrte_hip_set_gather_batch), both of which measured faster. */
 #define RRTE_FLAG_GATHER_OVERLAP 2u
 
 typedef struct rrte_render_params {
@@ -358,16 +358,31 @@ rrte_status rrte_hip_render_gather_async(rrte_ctx* ctx, const rrte_scene_ir* sce
                                          const rrte_render_params* params, int root,
                                          void* d_full_rgba8, void* stream);
 
+/* Collective failure detection (the reference has none: examples/basic-demo/src/main.rs:145-150
+ * only stops its loop).  Every host wait that covers a gather -- rrte_hip_synchronize, the blocking
+ * rrte_hip_render_gather, rrte_hip_comm_init's drain -- polls the work and ncclCommGetAsyncError
+ * instead of blocking; a gather that reports an error or does not complete within `ms` (default
+ * 30000; env RRTE_COMM_TIMEOUT_MS) aborts the communicator (ncclCommAbort) and returns
+ * RRTE_RCCL_ERROR with the reason in rrte_hip_last_error.  A failed gather of either form leaves the
+ * communicator aborted: every later gather call returns RRTE_RCCL_ERROR until rrte_hip_comm_init.
+ * (Fault injection for tests: env RRTE_FAULT_STALL_GATHER=N stalls the N-th collective of a context
+ * on the device until the host gives up on it -- a stalled peer seen from this rank.) */
+rrte_status rrte_hip_set_comm_timeout(rrte_ctx* ctx, uint32_t ms);
+
 /* Batched gather (throughput mode, SURVEY §8e "fewer, larger collectives"): with frames > 1 each
  * rrte_hip_render_gather_async only records the frame (its camera is read, the scene uploaded if it
  * changed) into the open batch; every `frames` frames the batch renders in multi-frame launches (up
  * to 8 frames per launch) on the context's render streams, after the work already queued on the
  * frames' streams, and ONE ncclGather on the context's comm stream moves all of them to the root,
  * which de-interleaves each into its d_full_rgba8.  A frame's d_full_rgba8 is then complete only
- * after rrte_hip_flush + a synchronisation of the device, or rrte_hip_synchronize (which flushes).
- * A frame of another size, band height, root, slab format, mode or sampling setup closes the open
- * batch, as do a scene change (any entry point) and a blocking rrte_hip_render_gather.  frames in
- * [1, 16]; every rank must use the same setting.  Flushing with no open batch does nothing. */
+ * after rrte_hip_flush + a synchronisation (rrte_hip_synchronize, or of the device).  Only gather-path
+ * calls every rank makes close a batch (collective): a full batch, rrte_hip_flush, rrte_hip_set_gather_batch,
+ * rrte_hip_comm_init, a blocking rrte_hip_render_gather, and a gather frame of another size, band
+ * height, root, slab format, mode or sampling setup.  Local calls never do: rrte_hip_synchronize and a
+ * scene change through rrte_hip_render / render_f32 / render_async only RENDER the open batch's
+ * frames (with the scene they were issued with) and leave its gather for the next collective close,
+ * so one rank may poll or render a preview on its own.  frames in [1, 16]; every rank must use the
+ * same setting.  Flushing with no open batch does nothing. */
 rrte_status rrte_hip_set_gather_batch(rrte_ctx* ctx, uint32_t frames);
 rrte_status rrte_hip_flush(rrte_ctx* ctx);
 

@@ -133,6 +133,7 @@ EXPORTS = {
     "rrte_hip_band_rows_for_rank": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_int, C.c_int]),
     "rrte_hip_set_gather_batch": (C.c_int, [_P, C.c_uint32]),
     "rrte_hip_flush": (C.c_int, [_P]),
+    "rrte_hip_set_comm_timeout": (C.c_int, [_P, C.c_uint32]),
 }
 
 _lib = None

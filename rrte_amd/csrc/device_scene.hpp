@@ -169,6 +169,54 @@ __device__ __forceinline__ float div_rn(float a, float b) {
     }
     return a / b;
 }
+// Lane select on a wave mask held in SGPRs: lane i gets `b` if bit i of m is set, else `a` -- one
+// v_cndmask_b32 reading the mask directly (what __builtin_amdgcn_inverse_ballot_w64 lowers to; the
+// hiprtc front end of this ROCm does not know that builtin).
+__device__ __forceinline__ float mask_select(uint64_t m, float a, float b) {
+    float r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+__device__ __forceinline__ bool mask_lane(uint64_t m) { return mask_select(m, 0.0f, 1.0f) != 0.0f; }
+
+// Guard policies of the SDF evaluation (ray_kernels.hpp: sdf_leaf ... SdfStaticProgram::eval).
+// GuardNow: sqrt_rn / div_rn as above, each with its own divergent fallback branch (an EXEC save,
+// branch and restore on the scalar unit per call).  GuardDefer: the same short sequences, but each
+// range test only folds into a running unsigned max of (bits - lower bound) -- one v_sub + v_max_u32,
+// nothing on the scalar unit -- and the caller tests bad() once per evaluation and re-evaluates the
+// flagged lanes with GuardSlow (the compiler's full sequences: bit-identical to the short ones
+// wherever those are in range, so any lane may take it).  A value is in range iff bits(x) - LO
+// <= SPAN as unsigned integers (positive floats order like their bit patterns; negatives and NaNs
+// wrap above), exactly the tests of sqrt_rn / div_rn.
+struct GuardNow {
+    __device__ __forceinline__ float sqrt(float x) { return sqrt_rn(x); }
+    __device__ __forceinline__ float div(float a, float b) { return div_rn(a, b); }
+};
+struct GuardSlow {
+    __device__ __forceinline__ float sqrt(float x) { return __builtin_sqrtf(x); }
+    __device__ __forceinline__ float div(float a, float b) { return a / b; }
+};
+struct GuardDefer {
+    static constexpr uint32_t kSqrtLo = 0x0F800000u, kSqrtSpan = 0x7F800000u - 0x0F800000u - 1u;  // [2^-96, FLT_MAX]
+    static constexpr uint32_t kDivLo = 0x21800000u, kDivSpan = 0x5D800000u - 0x21800000u;          // |a| in [2^-60, 2^60]
+    uint32_t sq = 0u, dv = 0u;
+    __device__ __forceinline__ float sqrt(float x) {
+        const float y = __builtin_amdgcn_rsqf(x);
+        const float s = x * y;
+        const float e = __builtin_fmaf(-s, s, x);
+        sq = __builtin_elementwise_max(sq, __float_as_uint(x) - kSqrtLo);
+        return __builtin_fmaf(e, 0.5f * y, s);
+    }
+    __device__ __forceinline__ float div(float a, float b) {
+        if (__builtin_constant_p(b) && __builtin_fabsf(b) >= 0x1.0p-60f && __builtin_fabsf(b) <= 0x1.0p+60f) {
+            dv = __builtin_elementwise_max(dv, __float_as_uint(__builtin_fabsf(a)) - kDivLo);
+            return div_by_rcp(a, b, 1.0f / b);
+        }
+        return a / b;
+    }
+    __device__ __forceinline__ bool bad() const { return sq > kSqrtSpan || dv > kDivSpan; }
+};
+
 __device__ __forceinline__ f3 vadd(f3 a, f3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ f3 vsub(f3 a, f3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ f3 vneg(f3 a) { return V(-a.x, -a.y, -a.z); }

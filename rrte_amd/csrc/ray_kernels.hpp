@@ -114,67 +114,72 @@ __device__ __forceinline__ void for_each_light(const S& sc, F&& f) {
 }
 
 // ------------------------------------------------------------- SDF program
-__device__ __forceinline__ float len2f(float a, float b) { return sqrt_rn(a * a + b * b); }
-__device__ __forceinline__ float len3f(float a, float b, float c) { return sqrt_rn((a * a + b * b) + c * c); }
+// The SDF evaluation is templated on its guard policy G (device_scene.hpp: GuardNow / GuardDefer /
+// GuardSlow) for its square roots and constant divides; every policy returns the same bits.
+template <class G>
+__device__ __forceinline__ float len2f(G& g, float a, float b) { return g.sqrt(a * a + b * b); }
+template <class G>
+__device__ __forceinline__ float len3f(G& g, float a, float b, float c) { return g.sqrt((a * a + b * b) + c * c); }
 
-__device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__ f, f3 p) {
+template <class G>
+__device__ __forceinline__ float sdf_leaf(G& g, uint32_t op, const float* __restrict__ f, f3 p) {
     f3 q = vsub(p, V(f[0], f[1], f[2]));
     switch (op) {
     case RRTE_SDF_SPHERE:
-        return len3f(q.x, q.y, q.z) - f[3];
+        return len3f(g, q.x, q.y, q.z) - f[3];
     case RRTE_SDF_BOX: {
         float dx = fabsf(q.x) - f[4] * 0.5f, dy = fabsf(q.y) - f[5] * 0.5f, dz = fabsf(q.z) - f[6] * 0.5f;
-        float outside = len3f(smx(dx, 0.0f), smx(dy, 0.0f), smx(dz, 0.0f));
+        float outside = len3f(g, smx(dx, 0.0f), smx(dy, 0.0f), smx(dz, 0.0f));
         float inside = smn(smx(dx, smx(dy, dz)), 0.0f);
         return outside + inside;
     }
     case RRTE_SDF_CYLINDER: {
-        float dx = len2f(q.x, q.z) - f[3], dy = fabsf(q.y) - f[4] * 0.5f;
-        return smn(smx(dx, dy), 0.0f) + len2f(smx(dx, 0.0f), smx(dy, 0.0f));
+        float dx = len2f(g, q.x, q.z) - f[3], dy = fabsf(q.y) - f[4] * 0.5f;
+        return smn(smx(dx, dy), 0.0f) + len2f(g, smx(dx, 0.0f), smx(dy, 0.0f));
     }
     case RRTE_SDF_PRISM: {
         float a = smx(fabsf(q.x) * 0.866025f + q.y * 0.5f, -q.y) - f[5] * 0.25f;
         return smx(fabsf(q.z) - f[6] * 0.5f, a);
     }
     case RRTE_SDF_TORUS: {
-        float qx = len2f(q.x, q.z) - f[3];
-        return len2f(qx, q.y) - f[4];
+        float qx = len2f(g, q.x, q.z) - f[3];
+        return len2f(g, qx, q.y) - f[4];
     }
     case RRTE_SDF_TUBE: {
-        float rad = len2f(q.x, q.z);
+        float rad = len2f(g, q.x, q.z);
         float mid = (f[3] + f[4]) * 0.5f, half = (f[3] - f[4]) * 0.5f;
         float dx = fabsf(rad - mid) - half, dy = fabsf(q.y) - f[5] * 0.5f;
-        return smn(smx(dx, dy), 0.0f) + len2f(smx(dx, 0.0f), smx(dy, 0.0f));
+        return smn(smx(dx, dy), 0.0f) + len2f(g, smx(dx, 0.0f), smx(dy, 0.0f));
     }
     case RRTE_SDF_RING: {
-        float qx = len2f(q.x, q.y) - f[3];
-        return len2f(qx, q.z) - f[4];
+        float qx = len2f(g, q.x, q.y) - f[3];
+        return len2f(g, qx, q.z) - f[4];
     }
     case RRTE_SDF_CONE: {
         float r1 = f[3], hh = f[4] * 0.5f;
-        float qx = len2f(q.x, q.z), qy = q.y;
+        float qx = len2f(g, q.x, q.z), qy = q.y;
         float k2x = -r1, k2y = hh * 2.0f;
         float cax = qx - smn(qx, (qy < 0.0f) ? r1 : 0.0f);
         float cay = fabsf(qy) - hh;
         float k1mqx = 0.0f - qx, k1mqy = hh - qy;
         float tnum = k1mqx * k2x + k1mqy * k2y;
         float tden = k2x * k2x + k2y * k2y;
-        float t = sclamp(div_rn(tnum, tden), 0.0f, 1.0f);
+        float t = sclamp(g.div(tnum, tden), 0.0f, 1.0f);
         float cbx = (qx - 0.0f) + k2x * t;
         float cby = (qy - hh) + k2y * t;
         float s = (cbx < 0.0f && cay < 0.0f) ? -1.0f : 1.0f;
         float da = cax * cax + cay * cay, db = cbx * cbx + cby * cby;
-        return s * sqrt_rn(smn(da, db));
+        return s * g.sqrt(smn(da, db));
     }
     case RRTE_SDF_CAPSULE: {
         float hh = f[4] * 0.5f;
         float y = q.y - sclamp(q.y, -hh, hh);
-        return len3f(q.x, y, q.z) - f[3];
+        return len3f(g, q.x, y, q.z) - f[3];
     }
     case RRTE_SDF_ELLIPSOID: {
         float rx = f[4], ry = f[5], rz = f[6];
-        float k0 = len3f(div_rn(q.x, rx), div_rn(q.y, ry), div_rn(q.z, rz));
-        float k1 = len3f(div_rn(q.x, rx * rx), div_rn(q.y, ry * ry), div_rn(q.z, rz * rz));
+        float k0 = len3f(g, g.div(q.x, rx), g.div(q.y, ry), g.div(q.z, rz));
+        float k1 = len3f(g, g.div(q.x, rx * rx), g.div(q.y, ry * ry), g.div(q.z, rz * rz));
         if (!(k1 > 0.0f)) return -smn(rx, smn(ry, rz));
         return k0 * (k0 - 1.0f) / k1;
     }
@@ -184,13 +189,15 @@ __device__ __forceinline__ float sdf_leaf(uint32_t op, const float* __restrict__
 }
 
 // smooth_min (README.md:485-488)
-__device__ __forceinline__ float smin(float a, float b, float k) {
-    float h = sclamp(0.5f + div_rn(0.5f * (b - a), k), 0.0f, 1.0f);
+template <class G>
+__device__ __forceinline__ float smin(G& g, float a, float b, float k) {
+    float h = sclamp(0.5f + g.div(0.5f * (b - a), k), 0.0f, 1.0f);
     float om = 1.0f - h;
     return (a * h + b * om) - (k * h) * om;
 }
 
-__device__ __forceinline__ f3 sdf_deform(uint32_t op, const uint32_t* __restrict__ iarg,
+template <class G>
+__device__ __forceinline__ f3 sdf_deform(G& g, uint32_t op, const uint32_t* __restrict__ iarg,
                                          const float* __restrict__ f, f3 p) {
     f3 c = V(f[0], f[1], f[2]);
     f3 q = vsub(p, c);
@@ -210,7 +217,7 @@ __device__ __forceinline__ f3 sdf_deform(uint32_t op, const uint32_t* __restrict
     case RRTE_SDF_TAPER: {
         uint32_t ax = iarg[0];
         uint32_t u = (ax + 1) % 3, w = (ax + 2) % 3;
-        float t = sclamp(div_rn(comp(q, ax) + f[5] * 0.5f, f[5]), 0.0f, 1.0f);
+        float t = sclamp(g.div(comp(q, ax) + f[5] * 0.5f, f[5]), 0.0f, 1.0f);
         float s = f[3] + (f[4] - f[3]) * t;
         q = setcomp(q, u, comp(q, u) / s);
         q = setcomp(q, w, comp(q, w) / s);
@@ -250,11 +257,12 @@ __device__ __forceinline__ f3 sdf_deform(uint32_t op, const uint32_t* __restrict
 // One postfix node applied to the value / point stacks (leaves push a
 // distance, CSG ops pop two and push one, deformers push the point and
 // replace it, POP_POINT restores it).
-__device__ __forceinline__ void sdf_node_step(const rrte_sdf_node& n, float* vs, f3* ps, uint32_t& sp, uint32_t& pp,
+template <class G>
+__device__ __forceinline__ void sdf_node_step(G& g, const rrte_sdf_node& n, float* vs, f3* ps, uint32_t& sp, uint32_t& pp,
                                               f3& p) {
     const uint32_t op = n.op;
     if (op < 32) {
-        vs[sp] = sdf_leaf(op, n.f, p);
+        vs[sp] = sdf_leaf(g, op, n.f, p);
         ++sp;
     } else if (op < 64) {
         float b = vs[sp - 1], a = vs[sp - 2], r;
@@ -263,9 +271,9 @@ __device__ __forceinline__ void sdf_node_step(const rrte_sdf_node& n, float* vs,
         case RRTE_SDF_UNION: r = smn(a, b); break;
         case RRTE_SDF_DIFFERENCE: r = smx(a, -b); break;
         case RRTE_SDF_INTERSECTION: r = smx(a, b); break;
-        case RRTE_SDF_SMOOTH_UNION: r = smin(a, b, k); break;
-        case RRTE_SDF_SMOOTH_DIFFERENCE: r = -smin(-a, b, k); break;
-        default: r = -smin(-a, -b, k); break;
+        case RRTE_SDF_SMOOTH_UNION: r = smin(g, a, b, k); break;
+        case RRTE_SDF_SMOOTH_DIFFERENCE: r = -smin(g, -a, b, k); break;
+        default: r = -smin(g, -a, -b, k); break;
         }
         sp -= 2;
         vs[sp] = r;
@@ -273,7 +281,7 @@ __device__ __forceinline__ void sdf_node_step(const rrte_sdf_node& n, float* vs,
     } else if (op < 96) {
         ps[pp] = p;
         ++pp;
-        p = sdf_deform(op, n.i, n.f, p);
+        p = sdf_deform(g, op, n.i, n.f, p);
     } else {
         --pp;
         p = ps[pp];
@@ -287,7 +295,8 @@ __device__ __forceinline__ void sdf_node_step(const rrte_sdf_node& n, float* vs,
 // difference: h computed with L is 1, so h(b) is 1 by monotone rounding, and with b >= L >= 0 the
 // formula reduces to a + 0 / -(-a + 0)).  Wave-uniform: taken only when every active lane may take
 // it, so the result never depends on the guard.
-__device__ __forceinline__ bool sdf_guard(const rrte_sdf_node& g, float a, f3 p, float& r) {
+template <class G>
+__device__ __forceinline__ bool sdf_guard(G& gp, const rrte_sdf_node& g, float a, f3 p, float& r) {
     const float dx = p.x - g.f[4], dy = p.y - g.f[5], dz = p.z - g.f[6];
     const float s = __builtin_amdgcn_sqrtf((dx * dx + dy * dy) + dz * dz);
     const float L = g.f[8] * (s - g.f[7]);
@@ -302,12 +311,12 @@ __device__ __forceinline__ bool sdf_guard(const rrte_sdf_node& g, float a, f3 p,
         r = a;
         break;
     case RRTE_SDF_SMOOTH_UNION:
-        ok = ok && sclamp(0.5f + div_rn(0.5f * (L - a), g.f[0]), 0.0f, 1.0f) == 1.0f;
+        ok = ok && sclamp(0.5f + gp.div(0.5f * (L - a), g.f[0]), 0.0f, 1.0f) == 1.0f;
         r = a + 0.0f;
         break;
     default: {  // RRTE_SDF_SMOOTH_DIFFERENCE: -smin(-a, b, k)
         const float na = -a;
-        ok = ok && sclamp(0.5f + div_rn(0.5f * (L - na), g.f[0]), 0.0f, 1.0f) == 1.0f;
+        ok = ok && sclamp(0.5f + gp.div(0.5f * (L - na), g.f[0]), 0.0f, 1.0f) == 1.0f;
         r = -(na + 0.0f);
         break;
     }
@@ -323,21 +332,26 @@ struct SdfProgram {
     static constexpr bool kSmall = false;
     const rrte_sdf_node* __restrict__ nodes;
     uint32_t count;
-    __device__ __forceinline__ float operator()(f3 p) const {
+    template <class G>
+    __device__ __forceinline__ float eval(f3 p, G& g) const {
         float vs[RRTE_SDF_MAX_STACK];
         f3 ps[RRTE_SDF_MAX_POINT_STACK];
         uint32_t sp = 0, pp = 0;
         for (uint32_t i = 0; i < count; ++i) {
             const uint32_t link = nodes[i].i[2];
             float r;
-            if (link != 0u && sdf_guard(nodes[link - 1u], vs[sp - 1], p, r)) {
+            if (link != 0u && sdf_guard(g, nodes[link - 1u], vs[sp - 1], p, r)) {
                 vs[sp - 1] = r;
                 i = link - 1u;  // continue after the op
                 continue;
             }
-            sdf_node_step(nodes[i], vs, ps, sp, pp, p);
+            sdf_node_step(g, nodes[i], vs, ps, sp, pp, p);
         }
         return vs[0];
+    }
+    __device__ __forceinline__ float operator()(f3 p) const {
+        GuardNow g;
+        return eval(p, g);
     }
 };
 
@@ -397,20 +411,20 @@ constexpr float sdf_leaf_scale(const rrte_sdf_node* n, uint32_t count) {
 // constexpr scene, unrolled at compile time; ops fold, stack slots become
 // fixed registers.  A guarded operand [I, J) becomes a uniform branch around
 // its straight-line code.
-template <class S, uint32_t FIRST, uint32_t I, uint32_t END, bool CHECK>
-__device__ __forceinline__ void sdf_static_range(float* vs, f3* ps, uint32_t& sp, uint32_t& pp, f3& p) {
+template <class S, uint32_t FIRST, uint32_t I, uint32_t END, bool CHECK, class G>
+__device__ __forceinline__ void sdf_static_range(G& gp, float* vs, f3* ps, uint32_t& sp, uint32_t& pp, f3& p) {
     if constexpr (I < END) {
         constexpr rrte_sdf_node n = S::nodes[FIRST + I];
         constexpr uint32_t link = n.i[2];
         if constexpr (CHECK && link != 0u) {
             constexpr rrte_sdf_node g = S::nodes[FIRST + link - 1u];
             float r;
-            if (sdf_guard(g, vs[sp - 1], p, r)) vs[sp - 1] = r;
-            else sdf_static_range<S, FIRST, I, link, false>(vs, ps, sp, pp, p);
-            sdf_static_range<S, FIRST, link, END, true>(vs, ps, sp, pp, p);
+            if (sdf_guard(gp, g, vs[sp - 1], p, r)) vs[sp - 1] = r;
+            else sdf_static_range<S, FIRST, I, link, false>(gp, vs, ps, sp, pp, p);
+            sdf_static_range<S, FIRST, link, END, true>(gp, vs, ps, sp, pp, p);
         } else {
-            sdf_node_step(n, vs, ps, sp, pp, p);
-            sdf_static_range<S, FIRST, I + 1u, END, true>(vs, ps, sp, pp, p);
+            sdf_node_step(gp, n, vs, ps, sp, pp, p);
+            sdf_static_range<S, FIRST, I + 1u, END, true>(gp, vs, ps, sp, pp, p);
         }
     }
 }
@@ -419,12 +433,17 @@ template <class S, uint32_t FIRST, uint32_t COUNT>
 struct SdfStaticProgram {
     static constexpr float kLeafScale = sdf_leaf_scale(S::nodes + FIRST, COUNT);
     static constexpr bool kSmall = COUNT <= 8u;
-    __device__ __forceinline__ float operator()(f3 p) const {
+    template <class G>
+    __device__ __forceinline__ float eval(f3 p, G& g) const {
         float vs[RRTE_SDF_MAX_STACK];
         f3 ps[RRTE_SDF_MAX_POINT_STACK];
         uint32_t sp = 0, pp = 0;
-        sdf_static_range<S, FIRST, 0u, COUNT, true>(vs, ps, sp, pp, p);
+        sdf_static_range<S, FIRST, 0u, COUNT, true>(g, vs, ps, sp, pp, p);
         return vs[0];
+    }
+    __device__ __forceinline__ float operator()(f3 p) const {
+        GuardNow g;
+        return eval(p, g);
     }
 };
 
@@ -466,8 +485,33 @@ __device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float
 #ifndef RRTE_MARCH_UNROLL
 #define RRTE_MARCH_UNROLL 1
 #endif
+#ifndef RRTE_MARCH_PRED
+#define RRTE_MARCH_PRED 0
+#endif
 #define RRTE_PRAGMA_(x) _Pragma(#x)
 #define RRTE_UNROLL_(n) RRTE_PRAGMA_(unroll n)
+// One SDF evaluation with deferred guards: the short sequences for every lane, one wave-uniform test
+// of the folded range checks, and the compiler's full sequences only when some lane needs them.
+#ifndef RRTE_DEFER_GUARDS
+#define RRTE_DEFER_GUARDS 0
+#endif
+template <class EVAL>
+__device__ __forceinline__ float eval_deferred(const EVAL& eval, f3 p) {
+#if RRTE_DEFER_GUARDS
+    GuardDefer g;
+    float d = eval.eval(p, g);
+    const uint64_t bad = __builtin_amdgcn_ballot_w64(g.bad());
+    if (__builtin_expect(bad != 0ull, 0)) {
+        GuardSlow gs;
+        const float ds = eval.eval(p, gs);
+        d = mask_select(bad, d, ds);
+    }
+    return d;
+#else
+    return eval(p);
+#endif
+}
+
 template <class EVAL, bool ANY = false, bool CONVEX = false>
 __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
                                           float& t_hit) {
@@ -491,6 +535,50 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     // t sequence and result as "if (d < eps*t) hit; t += d*scale; if (t > tend) miss" (NaN
     // included).  (A fully predicated form with a wave-uniform exit was measured slower.)
     bool hit = false;
+#if RRTE_MARCH_PRED
+    // Predicated march: the lanes that get here step together under one EXEC mask.  `live` (an SGPR
+    // lane mask) holds the lanes still marching; a lane that has stopped keeps its state through
+    // selects on that mask, the step counter is wave-uniform (SGPR), and the loop ends when no lane
+    // is left -- the same t sequence and result per lane as the divergent-exit loops below, without
+    // their per-step EXEC save / restore chains on the scalar unit.
+    {
+        uint64_t live = __builtin_amdgcn_ballot_w64(true);
+        [[maybe_unused]] float E = 0.0f, D3 = 0.0f, dp = __builtin_nanf(""), tp = t;
+        if constexpr (CONVEX) {
+            E = eps * (1.0f + 0x1p-20f);
+            constexpr float K = EVAL::kLeafScale;
+            D3 = 3.0f * 0x1p-17f *
+                 ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
+                  ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
+        }
+        // every condition as a wave mask (one v_cmp each, combined on the scalar unit)
+        uint64_t hitm = 0ull;
+        uint32_t left = steps;
+        if (left != 0u) {
+            for (;;) {
+                const f3 p = ray_at(r, t);
+                float d = eval_deferred(eval, p);
+                const float tn = t + d * scale;
+                const uint64_t hm = __builtin_amdgcn_ballot_w64(d < eps * t);
+                uint64_t sm = hm | __builtin_amdgcn_ballot_w64(tn > tend);
+                if constexpr (CONVEX) {
+                    sm |= __builtin_amdgcn_ballot_w64(d - E * t >= D3) &
+                          __builtin_amdgcn_ballot_w64((d - dp) - E * (t - tp) >= D3);
+                    dp = d;
+                    tp = t;
+                }
+                hitm |= hm & live;
+                t = mask_select(live & ~hm, t, tn);
+                live &= ~sm;
+                left = __builtin_amdgcn_readfirstlane(left - 1u);
+                if ((left == 0u) | (live == 0ull)) break;
+            }
+        }
+        hit = mask_lane(hitm);
+        t_hit = t;
+        return hit;
+    }
+#endif
     if constexpr (CONVEX) {
         const float E = eps * (1.0f + 0x1p-20f);
         constexpr float K = EVAL::kLeafScale;
@@ -534,25 +622,43 @@ RRTE_UNROLL_(RRTE_MARCH_UNROLL)
 template <class EVAL>
 __device__ __forceinline__ void sdf_hit_attributes(const EVAL& eval, const Ray& r, float t, Hit& out) {
     const float h = 1e-3f;
-    f3 p = ray_at(r, t), n = V(0.0f, 0.0f, 0.0f);
-    auto tap = [&](uint32_t k) {
-        bool sx = (k == 0) || (k == 3), sy = (k >= 2), sz = (k == 1) || (k == 3);
-        f3 q = V(sx ? p.x + h : p.x - h, sy ? p.y + h : p.y - h, sz ? p.z + h : p.z - h);
-        float d = eval(q);
-        if (k == 0) { n.x = d; n.y = -d; n.z = -d; }
-        else if (k == 1) { n.x = n.x - d; n.y = n.y - d; n.z = n.z + d; }
-        else if (k == 2) { n.x = n.x - d; n.y = n.y + d; n.z = n.z - d; }
-        else { n.x = n.x + d; n.y = n.y + d; n.z = n.z + d; }
-    };
-    if constexpr (EVAL::kSmall) {
-        // short programs (scene-specialised, <= 8 nodes): four straight-line taps, no per-tap selects
-        // or loop control (-1.3 % per headline frame; long programs keep the loop for code size)
+    const f3 p = ray_at(r, t);
+    auto taps = [&](auto& g) {
+        f3 n = V(0.0f, 0.0f, 0.0f);
+        auto tap = [&](uint32_t k) {
+            bool sx = (k == 0) || (k == 3), sy = (k >= 2), sz = (k == 1) || (k == 3);
+            f3 q = V(sx ? p.x + h : p.x - h, sy ? p.y + h : p.y - h, sz ? p.z + h : p.z - h);
+            float d = eval.eval(q, g);
+            if (k == 0) { n.x = d; n.y = -d; n.z = -d; }
+            else if (k == 1) { n.x = n.x - d; n.y = n.y - d; n.z = n.z + d; }
+            else if (k == 2) { n.x = n.x - d; n.y = n.y + d; n.z = n.z - d; }
+            else { n.x = n.x + d; n.y = n.y + d; n.z = n.z + d; }
+        };
+        if constexpr (EVAL::kSmall) {
+            // short programs (scene-specialised, <= 8 nodes): four straight-line taps, no per-tap selects
+            // or loop control (-1.3 % per headline frame; long programs keep the loop for code size)
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) tap(k);
-    } else {
+            for (uint32_t k = 0; k < 4; ++k) tap(k);
+        } else {
 #pragma unroll 1
-        for (uint32_t k = 0; k < 4; ++k) tap(k);
+            for (uint32_t k = 0; k < 4; ++k) tap(k);
+        }
+        return n;
+    };
+#if RRTE_DEFER_GUARDS
+    // deferred guards over the four taps: one wave-uniform test, the full sequences only if needed
+    GuardDefer g;
+    f3 n = taps(g);
+    const uint64_t bad = __builtin_amdgcn_ballot_w64(g.bad());
+    if (__builtin_expect(bad != 0ull, 0)) {
+        GuardSlow gs;
+        const f3 ns = taps(gs);
+        n = V(mask_select(bad, n.x, ns.x), mask_select(bad, n.y, ns.y), mask_select(bad, n.z, ns.z));
     }
+#else
+    GuardNow g;
+    const f3 n = taps(g);
+#endif
     hit_new(out, t, p, vnorm(n), r);
 }
 
@@ -1546,7 +1652,8 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
     }
     const float bias = kp.bias;
     // contribution of one light to a hit lane (light.rs illuminate + N.L + shadow ray)
-    auto shade = [&](const DLight& l, uint64_t smask) {
+    // RRTE_DEBUG bit 8 (timing diagnostics only, wrong images): shadow tests for light (debug >> 9) & 7 only
+    auto shade = [&](const DLight& l, uint64_t smask, uint32_t li) {
         Contrib k = illuminate(l, h.p);
         if (l.kind == RRTE_LIGHT_AMBIENT) {
             cr = cr + ar * k.cr;
@@ -1559,7 +1666,8 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             ++nshadow;
             Ray sr = ray_new_unit(vadd(h.p, vmuls(h.n, bias)), k.dir);
             // RRTE_DEBUG bit 6 (timing diagnostics only, wrong images): skip the object the ray starts on
-            if ((kp.debug & 1u) || !occluded(sc, sr, bias, k.dist, smask, (kp.debug & 64u) ? idx : -1)) {
+            if ((kp.debug & 1u) || ((kp.debug & 256u) && li != ((kp.debug >> 9) & 7u)) ||
+                !occluded(sc, sr, bias, k.dist, smask, (kp.debug & 64u) ? idx : -1)) {
                 float f = k.att * ndl;
                 cr = cr + ar * (k.cr * f);
                 cg = cg + ag * (k.cg * f);
@@ -1568,7 +1676,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
         }
     };
     if constexpr (!CULL) {
-        if (hit) for_each_light(sc, [&](auto lii) { shade(light_at(sc, lii), ~0ull); });
+        if (hit) for_each_light(sc, [&](auto lii) { shade(light_at(sc, lii), ~0ull, (uint32_t)lii); });
     } else {
         HitBound hb{};
         hb.unsafe = true;  // no bounds table: every mask all-ones
@@ -1583,14 +1691,14 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
                 auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii), bnd); };
                 static_for<0, S::num_lights>(cull_one);
             }
-            auto shade_one = [&](auto lii) { if (hit) shade(light_at(sc, lii), smask[(uint32_t)lii]); };
+            auto shade_one = [&](auto lii) { if (hit) shade(light_at(sc, lii), smask[(uint32_t)lii], (uint32_t)lii); };
             static_for<0, S::num_lights>(shade_one);
         } else {
             const float4 bnd = cull_on(cl) ? load_bound(cl) : float4{};
 #pragma unroll 1
             for (uint32_t li = 0; li < sc.num_lights; ++li) {
                 const uint64_t sm = shadow_cull(cl, hb, sc.lights[li], bnd);
-                if (hit) shade(sc.lights[li], sm);
+                if (hit) shade(sc.lights[li], sm, li);
             }
         }
     }

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <future>
+#include <thread>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -92,6 +93,7 @@ struct rrte_ctx {
     hipStream_t render_stream[kBatchSlabs] = {};
     struct Batch {
         uint32_t n = 0, cap = 0;             // frames planned into it / frames it was opened for
+        uint32_t rendered = 0;               // frames [0, rendered) already launched into the send slab
         uint32_t width = 0, height = 0, band = 0;
         int root = 0;
         bool rgb24 = false;
@@ -111,6 +113,20 @@ struct rrte_ctx {
     uint8_t* d_brecv[kBatchSlabs] = {};
     size_t cap_brecv[kBatchSlabs] = {};
     uint64_t gather_frames = 0;
+    // Collective failure detection: every wait for a gather is bounded by comm_timeout_ms
+    // and polls ncclCommGetAsyncError; a gather that fails or does not complete aborts the communicator
+    // (ncclCommAbort) and every later gather call returns RRTE_RCCL_ERROR until rrte_hip_comm_init.
+    uint32_t comm_timeout_ms = 30000;
+    bool comm_failed = false;
+    std::string comm_fail_msg;
+    uint64_t gathers_issued = 0;       // collectives issued on this communicator (both forms)
+    hipEvent_t ev_poll[3 + 3] = {};    // bounded waits: the context's streams + the last gather
+    // RRTE_FAULT_STALL_GATHER=N (fault injection, tests only): the N-th collective on this context is
+    // preceded on its stream by a kernel that spins until the host releases it (or 5 s pass) -- a
+    // stalled peer as seen from this rank.
+    uint64_t fault_stall_at = 0;
+    uint32_t* h_stall = nullptr;       // pinned, device-visible release flag
+    bool stall_armed = false;
     rrte_stats stats{};
     bool pending_kernel_timing = false;
     uint64_t pending_primary = 0;
@@ -146,6 +162,8 @@ struct rrte_ctx {
 };
 
 static rrte_status flush_batch(rrte_ctx* c);
+static rrte_status render_batch(rrte_ctx* c);
+static rrte_status wait_bounded(rrte_ctx* c);
 
 namespace {
 
@@ -482,9 +500,11 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     scene_key_parts(s, kparts);
     const size_t key_len = kparts.total;
     const bool same = scene_same(c, s);
-    if (!same && c->batch.n) {
-        // the open batch renders the cached scene at its flush: render it before the scene changes
-        rrte_status r = flush_batch(c);
+    if (!same && c->batch.rendered < c->batch.n) {
+        // the open batch's frames render the cached scene: launch them before the scene changes.  Local
+        // only (no gather): a rank's own preview render with another scene must not close a batch the
+        // other ranks keep open
+        rrte_status r = render_batch(c);
         if (r != RRTE_OK) return r;
     }
     *upload_ms = 0.0;
@@ -957,6 +977,8 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_DIAG_SKIP")) c->env_diag_skip = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GATHER_RGB24")) c->env_gather_rgba = g[0] == '0';
     c->env_guard_leaves = env_guard_setting();
+    if (const char* g = getenv("RRTE_COMM_TIMEOUT_MS")) c->comm_timeout_ms = std::max<uint32_t>(1u, (uint32_t)strtoul(g, nullptr, 0));
+    if (const char* g = getenv("RRTE_FAULT_STALL_GATHER")) c->fault_stall_at = strtoull(g, nullptr, 0);
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
@@ -980,6 +1002,11 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if ((e = hipMemset(c->d_counters, 0, kCounterBytes)) != hipSuccess) return bail(e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_counters), kCounterBytes, hipHostMallocDefault)) != hipSuccess) return bail(e);
     memset(c->h_counters, 0, kCounterBytes);
+    if (c->fault_stall_at) {
+        if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_stall), 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+            return bail(e);
+        *c->h_stall = 1u;
+    }
     *out = c;
     return RRTE_OK;
 }
@@ -994,6 +1021,7 @@ void rrte_hip_destroy(rrte_ctx* c) {
         fprintf(stderr, "\n");
     }
     (void)hipSetDevice(c->device);
+    if (c->h_stall) __hip_atomic_store(c->h_stall, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // injected stall
     (void)hipDeviceSynchronize();  // frames may still run on caller streams
     if (c->comm) ncclCommDestroy(c->comm);
     c->jit_pending.clear();  // joins background compiles
@@ -1006,6 +1034,9 @@ void rrte_hip_destroy(rrte_ctx* c) {
     for (uint32_t* b : c->d_slab)
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->h_stall) (void)hipHostFree(c->h_stall);
+    for (hipEvent_t e : c->ev_poll)
+        if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -1073,10 +1104,20 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
 
 rrte_status rrte_hip_synchronize(rrte_ctx* c) {
     if (!c) return RRTE_INVALID_ARG;
-    rrte_status r = flush_batch(c);
+    HIPCHK(c, hipSetDevice(c->device));
+    // local: an open gather batch is rendered but stays open (its gather is collective: rrte_hip_flush)
+    rrte_status r = render_batch(c);
     if (r != RRTE_OK) return r;
+    if ((r = wait_bounded(c)) != RRTE_OK) return r;
     HIPCHK(c, hipDeviceSynchronize());
     return finish_frame(c);
+}
+
+rrte_status rrte_hip_set_comm_timeout(rrte_ctx* c, uint32_t ms) {
+    if (!c) return RRTE_INVALID_ARG;
+    if (ms == 0) return fail(c, RRTE_INVALID_ARG, "comm timeout must be > 0 ms");
+    c->comm_timeout_ms = ms;
+    return RRTE_OK;
 }
 
 rrte_status rrte_hip_query(rrte_ctx* c, uint32_t* busy) {
@@ -1194,12 +1235,20 @@ rrte_status rrte_hip_comm_unique_id(uint8_t out_id[RRTE_UNIQUE_ID_BYTES]) {
 rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t id_bytes[RRTE_UNIQUE_ID_BYTES]) {
     if (!c || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return fail(c, RRTE_INVALID_ARG, "bad comm args");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipDeviceSynchronize());  // no gather of the old communicator may still run
+    // frames already accepted into an open batch are gathered on the old communicator first (every rank
+    // re-initialises together, so this collective matches); then nothing of the old one may still run
+    rrte_status fr = c->comm ? flush_batch(c) : RRTE_OK;
+    c->batch.n = c->batch.nsrc = c->batch.rendered = 0;
+    if (fr == RRTE_OK && c->comm) fr = wait_bounded(c);
+    HIPCHK(c, hipDeviceSynchronize());
     if (c->comm) ncclCommDestroy(c->comm);
     c->comm = nullptr;
-    c->batch.n = 0;
     c->last_gather_stream = nullptr;
     c->last_gather_ev = nullptr;
+    c->comm_failed = false;
+    c->comm_fail_msg.clear();
+    c->gathers_issued = 0;
+    if (fr != RRTE_OK) return fr;
     ncclUniqueId id;
     memcpy(&id, id_bytes, sizeof id);
     NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
@@ -1250,12 +1299,15 @@ static rrte_status deinterleave(rrte_ctx* c, hipStream_t st, const uint8_t* gath
     return RRTE_OK;
 }
 
-static rrte_status flush_batch(rrte_ctx* c) {
+// Launch the open batch's frames that have not been rendered yet ([rendered, n)) into its send slab on
+// the slab's render stream, after the work queued on the frames' caller streams.  Local: no
+// collective, so a rank may call it on its own (a scene change through a non-gather entry point,
+// rrte_hip_synchronize) without desynchronising the ranks' gathers.
+static rrte_status render_batch(rrte_ctx* c) {
     rrte_ctx::Batch& b = c->batch;
-    if (b.n == 0) return RRTE_OK;
+    if (b.rendered >= b.n) return RRTE_OK;
     HostSection hs(c);
     const int k = c->bslot;
-    const size_t count = (size_t)b.n * b.slice;  // bytes per rank
     hipStream_t rs = c->render_stream[k];
     // the renders follow the frames' caller streams (scene uploads, the callers' own prior work) and
     // the slab's previous batch (its gather reads the send slab)
@@ -1264,9 +1316,9 @@ static rrte_status flush_batch(rrte_ctx* c) {
             HIPCHK(c, hipEventRecord(b.ev_src[i], b.src[i]));
             HIPCHK(c, hipStreamWaitEvent(rs, b.ev_src[i], 0));
         }
-    HIPCHK(c, hipStreamWaitEvent(rs, c->ev_batch[k], 0));
+    if (b.rendered == 0) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_batch[k], 0));
     hs.lap(2);
-    for (uint32_t j0 = 0; j0 < b.n; j0 += kMaxLaunchFrames) {
+    for (uint32_t j0 = b.rendered; j0 < b.n; j0 += kMaxLaunchFrames) {
         const uint32_t nf = std::min<uint32_t>(b.n - j0, kMaxLaunchFrames);
         LaunchPlan& L = b.plan;
         memcpy(L.k.cam, b.cam + j0, nf * sizeof(FrameCam));
@@ -1276,29 +1328,148 @@ static rrte_status flush_batch(rrte_ctx* c) {
         rrte_status r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, rs);
         if (r != RRTE_OK) return r;
     }
+    b.rendered = b.n;
     HIPCHK(c, hipEventRecord(c->ev_render[k], rs));
     hs.lap(3);
-    HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
-    if (c->last_gather_stream && c->last_gather_stream != c->comm_stream)
-        HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->last_gather_ev, 0));
-    hs.lap(4);
-    if (!(c->env_diag_skip & 1u))
-        NCCLCHK(c, ncclGather(c->d_bsend[k], c->d_brecv[k], count, ncclUint8, b.root, c->comm, c->comm_stream));
-    hs.lap(5);
-    if (c->rank == b.root && !(c->env_diag_skip & 2u)) {
-        DeinterleaveTargets t{};
-        for (uint32_t j = 0; j < b.n; ++j) t.full[j] = b.full[j];
-        rrte_status r = deinterleave(c, c->comm_stream, c->d_brecv[k], t, b.n, b.width, b.height, b.band, b.rgb24,
-                                     count, b.slice);
-        if (r != RRTE_OK) return r;
+    return RRTE_OK;
+}
+
+// The stalled-peer stand-in of RRTE_FAULT_STALL_GATHER: spins on a host-written flag (vector atomic
+// loads at system scope) with its own 5 s deadline on the 100 MHz wall clock, so it always ends.
+__global__ void stall_kernel(const uint32_t* flag) {
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u &&
+           wall_clock64() - t0 < 500000000ull) {
+        __builtin_amdgcn_s_sleep(10);
     }
-    hs.lap(6);
-    HIPCHK(c, hipEventRecord(c->ev_batch[k], c->comm_stream));
+}
+
+// Before a collective on `st`: count it, and enqueue the injected stall if this is the one.
+static rrte_status before_collective(rrte_ctx* c, hipStream_t st) {
+    ++c->gathers_issued;
+    if (c->fault_stall_at && c->gathers_issued == c->fault_stall_at && c->h_stall) {
+        __hip_atomic_store(c->h_stall, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t* dflag = nullptr;
+        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&dflag), c->h_stall, 0));
+        hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, st, dflag);
+        HIPCHK(c, hipGetLastError());
+        c->stall_armed = true;
+        c->fault_stall_at = 0;  // one-shot
+    }
+    return RRTE_OK;
+}
+
+// A gather failed or did not finish in time: release any injected stall, give the queued work a short
+// bounded chance to drain (so nothing of this communicator is still running when it is torn down),
+// abort the communicator and fail every later gather call until rrte_hip_comm_init.
+static rrte_status comm_abort(rrte_ctx* c, const char* why) {
+    if (c->stall_armed && c->h_stall) __hip_atomic_store(c->h_stall, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    c->stall_armed = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        bool busy = false;
+        for (hipEvent_t e : c->ev_poll)
+            if (e && hipEventQuery(e) == hipErrorNotReady) busy = true;
+        if (!busy || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2000)) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    if (c->comm) (void)ncclCommAbort(c->comm);
+    c->comm = nullptr;
+    c->comm_failed = true;
+    c->comm_fail_msg = why;
+    rrte_ctx::Batch& b = c->batch;
+    b.n = b.nsrc = b.rendered = 0;
+    c->last_gather_stream = nullptr;
+    c->last_gather_ev = nullptr;
+    return fail(c, RRTE_RCCL_ERROR, "%s; communicator aborted (call rrte_hip_comm_init again)", why);
+}
+
+// Bounded wait for the context's own streams and its last gather: polls the events (and, while a
+// communicator exists, ncclCommGetAsyncError) instead of blocking, so a gather that never completes
+// -- a dead or stalled peer -- surfaces as RRTE_RCCL_ERROR after comm_timeout_ms instead of a hang.
+static rrte_status wait_bounded(rrte_ctx* c) {
+    hipStream_t ss[6] = {c->stream, c->comm_stream, c->render_stream[0], c->render_stream[1], c->render_stream[2],
+                         c->last_gather_stream};
+    static_assert(sizeof(c->ev_poll) / sizeof(c->ev_poll[0]) == 6, "poll events");
+    int n = 0;
+    for (int i = 0; i < 6; ++i) {
+        if (!ss[i]) continue;
+        if (!c->ev_poll[n]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_poll[n], hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->ev_poll[n], ss[i]));
+        ++n;
+    }
+    const bool watch = c->comm != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        bool busy = false;
+        for (int i = 0; i < n; ++i) {
+            const hipError_t e = hipEventQuery(c->ev_poll[i]);
+            if (e == hipErrorNotReady) {
+                busy = true;
+                break;
+            }
+            HIPCHK(c, e);
+        }
+        if (!busy) return RRTE_OK;
+        if (watch) {
+            ncclResult_t ae = ncclSuccess;
+            if (ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                char why[256];
+                snprintf(why, sizeof why, "RCCL asynchronous error: %s", ncclGetErrorString(ae));
+                return comm_abort(c, why);
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->comm_timeout_ms)) {
+                char why[256];
+                snprintf(why, sizeof why, "gather did not complete within %u ms (stalled or dead peer?)", c->comm_timeout_ms);
+                return comm_abort(c, why);
+            }
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+// Close the open batch (collective: every rank holds the same open batch -- same frames in the same
+// order -- so the ncclGather matches): render what is not rendered yet, then ONE ncclGather on the
+// comm stream moves every frame's slices to the root, which de-interleaves each into its caller
+// buffer.  Any failure resets the batch and aborts the communicator: a half-issued batch would leave
+// the ranks' collectives out of step.
+static rrte_status flush_batch(rrte_ctx* c) {
+    rrte_ctx::Batch& b = c->batch;
+    if (b.n == 0) return RRTE_OK;
+    if (c->comm_failed || !c->comm) {
+        b.n = b.nsrc = b.rendered = 0;
+        return fail(c, RRTE_RCCL_ERROR, "gather batch dropped: %s", c->comm_failed ? c->comm_fail_msg.c_str() : "no communicator");
+    }
+    rrte_status r = render_batch(c);
+    if (r != RRTE_OK) return comm_abort(c, ("batch render failed: " + c->err).c_str());
+    HostSection hs(c);
+    const int k = c->bslot;
+    const size_t count = (size_t)b.n * b.slice;  // bytes per rank
+    auto issue = [&]() -> rrte_status {
+        HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
+        if (c->last_gather_stream && c->last_gather_stream != c->comm_stream)
+            HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->last_gather_ev, 0));
+        hs.lap(4);
+        if ((r = before_collective(c, c->comm_stream)) != RRTE_OK) return r;
+        if (!(c->env_diag_skip & 1u))
+            NCCLCHK(c, ncclGather(c->d_bsend[k], c->d_brecv[k], count, ncclUint8, b.root, c->comm, c->comm_stream));
+        hs.lap(5);
+        if (c->rank == b.root && !(c->env_diag_skip & 2u)) {
+            DeinterleaveTargets t{};
+            for (uint32_t j = 0; j < b.n; ++j) t.full[j] = b.full[j];
+            if ((r = deinterleave(c, c->comm_stream, c->d_brecv[k], t, b.n, b.width, b.height, b.band, b.rgb24, count,
+                                  b.slice)) != RRTE_OK)
+                return r;
+        }
+        hs.lap(6);
+        HIPCHK(c, hipEventRecord(c->ev_batch[k], c->comm_stream));
+        return RRTE_OK;
+    };
+    if ((r = issue()) != RRTE_OK) return comm_abort(c, ("batch gather failed: " + c->err).c_str());
     c->last_gather_stream = c->comm_stream;
     c->last_gather_ev = c->ev_batch[k];
     c->bslot = (k + 1) % rrte_ctx::kBatchSlabs;
-    b.n = 0;
-    b.nsrc = 0;
+    b.n = b.nsrc = b.rendered = 0;
     hs.lap(7);
     return RRTE_OK;
 }
@@ -1335,6 +1506,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         if (timing) HIPCHK(c, hipEventRecord(c->ev1, st));
         return r;
     }
+    if (c->comm_failed) return fail(c, RRTE_RCCL_ERROR, "communicator aborted earlier (%s); call rrte_hip_comm_init", c->comm_fail_msg.c_str());
     if (!c->comm) return fail(c, RRTE_INVALID_ARG, "rrte_hip_comm_init has not been called");
     if (c->gather_batch > 1 && !timing) {
         rrte_ctx::Batch& b = c->batch;
@@ -1411,12 +1583,21 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         if (c->last_gather_stream && c->last_gather_stream != st)
             HIPCHK(c, hipStreamWaitEvent(st, c->last_gather_ev, 0));
         hs.lap(4);
-        NCCLCHK(c, ncclGather(mine, slab, slice, ncclUint8, root, c->comm, st));
+        if ((r = before_collective(c, st)) != RRTE_OK) return comm_abort(c, ("gather setup failed: " + c->err).c_str());
+        {
+            const ncclResult_t nr = ncclGather(mine, slab, slice, ncclUint8, root, c->comm, st);
+            if (nr != ncclSuccess) {
+                char why[256];
+                snprintf(why, sizeof why, "ncclGather failed: %s", ncclGetErrorString(nr));
+                return comm_abort(c, why);
+            }
+        }
         hs.lap(5);
         if (c->rank == root) {
             DeinterleaveTargets t{};
             t.full[0] = static_cast<uint32_t*>(d_full);
-            if ((r = deinterleave(c, st, slab, t, 1, p->width, p->height, band, rgb24, slice, 0)) != RRTE_OK) return r;
+            if ((r = deinterleave(c, st, slab, t, 1, p->width, p->height, band, rgb24, slice, 0)) != RRTE_OK)
+                return comm_abort(c, ("de-interleave failed: " + c->err).c_str());
         }
         hs.lap(6);
         HIPCHK(c, hipEventRecord(c->ev_gath[slot], st));
@@ -1470,6 +1651,7 @@ rrte_status rrte_hip_render_gather(rrte_ctx* c, const rrte_scene_ir* s, const rr
     if ((r = gather_frame(c, s, p, root, full, c->stream, true)) != RRTE_OK) return r;
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     if (c->rank == root && out) HIPCHK(c, hipMemcpyAsync(out, full, npix * 4, hipMemcpyDeviceToHost, c->stream));
+    if ((r = wait_bounded(c)) != RRTE_OK) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float k_ms = 0.0f, all_ms = 0.0f;
     if (c->nranks > 1) {

@@ -6,7 +6,12 @@ the same inputs.  It restates (paths relative to Melthizar/RRTE):
   raytracer.rs:45-148 (render/ray_color, REFCOMPAT depth 1), camera.rs:98-117,
   primitives.rs:57-725 (all seven intersectors), light.rs:170-194, color.rs:48-113,
 and the build-defined LAMBERT_SHADOW pass and SDF leaf/CSG formulas.
-It is written from the reference source, not from the C oracle.
+It is written from the reference source, not from the C oracle.  The SDF half (README.md:458-510
+signatures; formulas build-defined in DESIGN.md §6) covers all 10 leaves, the 6 CSG ops with
+README.md:485-488's smooth_min, Bend/Twist/Taper/Noise/Wave deformers and their chaining (the point
+stack of include/rrte_hip.h's postfix program), the bounded sphere-tracing march and the tetrahedral
+normal -- written from DESIGN.md §6's definitions, with none of the device's exact shortcuts (CSG
+guards, convex secant exits, leaving-sphere early-outs), so agreement also checks those.
 """
 from __future__ import annotations
 
@@ -130,13 +135,20 @@ def _local(pr, o, d):
     return m, lo, ld
 
 
-def intersect(pr, o, d, tmin, tmax):
-    """SceneObject::intersect for one prim over all rays; returns a Hits record."""
+def intersect(pr, o, d, tmin, tmax, nodes=None):
+    """SceneObject::intersect for one prim over all rays; returns a Hits record.  `tmax` may be a
+    per-ray array (SDF objects march only up to the current closest hit); `nodes` is the scene's
+    SDF node array (SDF prims)."""
     n = o[0].shape[0]
     h = Hits(n)
     p = [F(v) for v in pr.p]
     with np.errstate(all="ignore"):
-        if pr.kind == abi.PRIM_SPHERE:
+        if pr.kind == abi.PRIM_SDF:
+            prog = [nodes[pr.sdf_first + k] for k in range(pr.sdf_count)]
+            ok, t = sdf_march(pr, prog, o, d, tmin, tmax)
+            pt, nn = sdf_attributes(prog, o, d, t)
+            h.set(ok, t, pt, nn, d)
+        elif pr.kind == abi.PRIM_SPHERE:
             c = p[0:3]
             oc = [o[k] - c[k] for k in range(3)]
             a = dot(d, d)
@@ -276,9 +288,10 @@ def intersect(pr, o, d, tmin, tmax):
     return h
 
 
-def render(scene: "abi.SceneIR", params: "abi.RenderParams"):
-    """REFCOMPAT (max_depth 1) or LAMBERT_SHADOW with analytic prims and point lights,
-    pixel-centre jitter, spp 1.  Returns (rgba8 HxWx4, f32 HxWx4, shadow_rays)."""
+def render(scene: "abi.SceneIR", params: "abi.RenderParams", linear=False):
+    """REFCOMPAT (max_depth 1) or LAMBERT_SHADOW with analytic and SDF prims and point lights,
+    pixel-centre jitter, spp 1.  Returns (rgba8 HxWx4, f32 HxWx4, shadow_rays); linear=True: the
+    f32 image is the averaged linear colour (pre-gamma, unclamped; RRTE_FLAG_F32_LINEAR)."""
     W, H = params.width, params.height
     assert params.samples_per_pixel == 1 and params.jitter == abi.JITTER_CENTER
     ys, xs = np.mgrid[0:H, 0:W]
@@ -296,8 +309,12 @@ def render(scene: "abi.SceneIR", params: "abi.RenderParams"):
     prims = [scene.prims[i] for i in range(scene.num_prims)]
     best = Hits(n)
     idx = np.full(n, -1)
+    nodes = [scene.sdf_nodes[i] for i in range(scene.num_sdf_nodes)]
     for i, pr in enumerate(prims):
-        h = intersect(pr, o, d, F(params.t_min), INF)
+        # raytracer.rs:103-113: analytic objects get t_max = INFINITY; SDF objects (build-defined)
+        # march only up to the closest hit so far
+        tmax = np.where(best.ok, best.t, INF) if pr.kind == abi.PRIM_SDF else INF
+        h = intersect(pr, o, d, F(params.t_min), tmax, nodes)
         better = h.ok & (~best.ok | (h.t < best.t))
         best.t = np.where(better, h.t, best.t)
         for k in range(3):
@@ -336,7 +353,7 @@ def render(scene: "abi.SceneIR", params: "abi.RenderParams"):
                 sorg = [best.p[k] + best.n[k] * bias for k in range(3)]
                 occ = np.zeros(n, bool)
                 for pr in prims:
-                    hs = intersect(pr, sorg, so, bias, dist)
+                    hs = intersect(pr, sorg, so, bias, dist, nodes)
                     occ |= hs.ok
                 lit = cast & ~occ
                 fct = att * ndl
@@ -351,6 +368,8 @@ def render(scene: "abi.SceneIR", params: "abi.RenderParams"):
         # render(): color = BLACK + sample (alpha starts at 1), then * (1/spp) (raytracer.rs:64-76)
         col = [(F(0) if k < 3 else F(1)) + col[k] for k in range(4)]
         col = [c * F(1.0) for c in col]
+        if linear:
+            return None, np.stack(col, -1).reshape(H, W, 4), shadow
         inv_g = F(1) / F(params.gamma)
         g = [np.power(col[k], inv_g) if k < 3 else col[k] for k in range(4)]
         g = [np.where(np.isnan(x), x, np.clip(x, F(0), F(1))) for x in g]
@@ -363,42 +382,249 @@ def render(scene: "abi.SceneIR", params: "abi.RenderParams"):
     return rgba8, f32, shadow
 
 
-# ------------------------------------------------------------ SDF formulas
+# ------------------------------------------------------------ SDF path
+def _mx(a, b):
+    """IEEE maxNum (a NaN operand yields the other): the SDF max."""
+    return np.fmax(a, b)
+
+
+def _mn(a, b):
+    return np.fmin(a, b)
+
+
+def _clamp(x, lo, hi):
+    return _mn(_mx(x, lo), hi)
+
+
+def _l2(a, b):
+    return np.sqrt(a * a + b * b)
+
+
+def _l3(a, b, c):
+    return np.sqrt((a * a + b * b) + c * c)
+
+
 def sdf_leaf(op, f, p):
+    """The ten leaves, local q = p - centre (DESIGN.md §6 'Primitives'; sizes are full extents)."""
     f = [F(x) for x in f]
     q = [p[k] - f[k] for k in range(3)]
-    l2 = lambda a, b: np.sqrt(a * a + b * b)  # noqa: E731
-    l3 = lambda a, b, c: np.sqrt((a * a + b * b) + c * c)  # noqa: E731
-    # SDF min/max are IEEE minNum/maxNum (a NaN operand yields the other): np.fmax / np.fmin
-    mx, mn = np.fmax, np.fmin
-    Z = F(0)
+    Z, H = F(0), F(0.5)
     if op == abi.SDF_SPHERE:
-        return l3(*q) - f[3]
-    if op == abi.SDF_BOX:
-        dx, dy, dz = np.abs(q[0]) - f[4] * F(.5), np.abs(q[1]) - f[5] * F(.5), np.abs(q[2]) - f[6] * F(.5)
-        return l3(mx(dx, Z), mx(dy, Z), mx(dz, Z)) + mn(mx(dx, mx(dy, dz)), Z)
-    if op == abi.SDF_CYLINDER:
-        dx, dy = l2(q[0], q[2]) - f[3], np.abs(q[1]) - f[4] * F(.5)
-        return mn(mx(dx, dy), Z) + l2(mx(dx, Z), mx(dy, Z))
-    if op == abi.SDF_TORUS:
-        return l2(l2(q[0], q[2]) - f[3], q[1]) - f[4]
-    if op == abi.SDF_RING:
-        return l2(l2(q[0], q[1]) - f[3], q[2]) - f[4]
-    if op == abi.SDF_CAPSULE:
-        hh = f[4] * F(.5)
-        y = q[1] - mn(mx(q[1], -hh), hh)
-        return l3(q[0], y, q[2]) - f[3]
-    if op == abi.SDF_TUBE:
-        rad = l2(q[0], q[2])
-        mid, half = (f[3] + f[4]) * F(.5), (f[3] - f[4]) * F(.5)
-        dx, dy = np.abs(rad - mid) - half, np.abs(q[1]) - f[5] * F(.5)
-        return mn(mx(dx, dy), Z) + l2(mx(dx, Z), mx(dy, Z))
+        return _l3(*q) - f[3]
+    if op == abi.SDF_BOX:  # exact box
+        dx, dy, dz = np.abs(q[0]) - f[4] * H, np.abs(q[1]) - f[5] * H, np.abs(q[2]) - f[6] * H
+        return _l3(_mx(dx, Z), _mx(dy, Z), _mx(dz, Z)) + _mn(_mx(dx, _mx(dy, dz)), Z)
+    if op == abi.SDF_CYLINDER:  # Y axis, capped, exact
+        dx, dy = _l2(q[0], q[2]) - f[3], np.abs(q[1]) - f[4] * H
+        return _mn(_mx(dx, dy), Z) + _l2(_mx(dx, Z), _mx(dy, Z))
+    if op == abi.SDF_PRISM:  # max(|q.z| - d/2, max(|q.x| 0.866025 + q.y/2, -q.y) - s_y/4)
+        a = _mx(np.abs(q[0]) * F(0.866025) + q[1] * H, -q[1]) - f[5] * F(0.25)
+        return _mx(np.abs(q[2]) - f[6] * H, a)
+    if op == abi.SDF_TORUS:  # XZ ring
+        return _l2(_l2(q[0], q[2]) - f[3], q[1]) - f[4]
+    if op == abi.SDF_TUBE:  # annulus, capped
+        rad = _l2(q[0], q[2])
+        mid, half = (f[3] + f[4]) * H, (f[3] - f[4]) * H
+        dx, dy = np.abs(rad - mid) - half, np.abs(q[1]) - f[5] * H
+        return _mn(_mx(dx, dy), Z) + _l2(_mx(dx, Z), _mx(dy, Z))
+    if op == abi.SDF_RING:  # XY ring
+        return _l2(_l2(q[0], q[1]) - f[3], q[2]) - f[4]
+    if op == abi.SDF_CONE:
+        # capped cone, base radius r at y = -h/2, apex at +h/2: distance to the nearer of the base
+        # disc's rim segment ca and the slanted side segment cb (from the apex (0, h/2) along
+        # k2 = (-r, h)), negative inside
+        r1, hh = f[3], f[4] * H
+        qx, qy = _l2(q[0], q[2]), q[1]
+        k2x, k2y = -r1, hh * F(2)
+        cax = qx - _mn(qx, np.where(qy < Z, r1, Z))
+        cay = np.abs(qy) - hh
+        t = _clamp(((Z - qx) * k2x + (hh - qy) * k2y) / (k2x * k2x + k2y * k2y), Z, F(1))
+        cbx = (qx - Z) + k2x * t
+        cby = (qy - hh) + k2y * t
+        sgn = np.where((cbx < Z) & (cay < Z), F(-1), F(1))
+        return sgn * np.sqrt(_mn(cax * cax + cay * cay, cbx * cbx + cby * cby))
+    if op == abi.SDF_CAPSULE:  # segment on Y
+        hh = f[4] * H
+        y = q[1] - _mn(_mx(q[1], -hh), hh)
+        return _l3(q[0], y, q[2]) - f[3]
+    if op == abi.SDF_ELLIPSOID:  # k0 (k0 - 1) / k1 bound
+        rx, ry, rz = f[4], f[5], f[6]
+        k0 = _l3(q[0] / rx, q[1] / ry, q[2] / rz)
+        k1 = _l3(q[0] / (rx * rx), q[1] / (ry * ry), q[2] / (rz * rz))
+        return np.where(k1 > Z, k0 * (k0 - F(1)) / k1, -_mn(rx, _mn(ry, rz)))
     raise NotImplementedError(op)
 
 
 def smin(a, b, k):
+    """README.md:485-488 smooth_min, evaluated left to right as written."""
     k = F(k)
-    h = (F(0.5) + (F(0.5) * (b - a)) / k)
-    h = np.fmin(np.fmax(h, F(0)), F(1))
+    h = _clamp(F(0.5) + (F(0.5) * (b - a)) / k, F(0), F(1))
     om = F(1) - h
     return (a * h + b * om) - (k * h) * om
+
+
+def csg(op, a, b, k):
+    """CSGOperation (README.md:471-482): union min, difference max(a, -b), intersection max; the
+    smooth forms through smooth_min: difference -smin(-a, b), intersection -smin(-a, -b)."""
+    if op == abi.SDF_UNION:
+        return _mn(a, b)
+    if op == abi.SDF_DIFFERENCE:
+        return _mx(a, -b)
+    if op == abi.SDF_INTERSECTION:
+        return _mx(a, b)
+    if op == abi.SDF_SMOOTH_UNION:
+        return smin(a, b, k)
+    if op == abi.SDF_SMOOTH_DIFFERENCE:
+        return -smin(-a, b, k)
+    if op == abi.SDF_SMOOTH_INTERSECTION:
+        return -smin(-a, -b, k)
+    raise NotImplementedError(op)
+
+
+# build-defined sin/cos (DESIGN.md §6): 3-part Cody-Waite reduction by pi/2, minimax polynomials
+_TWO_OVER_PI = F(0.636619772)
+_PIO2 = (F(1.5703125), F(4.837512969970703125e-4), F(7.549789948768648e-8))
+_SIN = (F(-1.6666654611e-1), F(8.3321608736e-3), F(-1.9515295891e-4))
+_COS = (F(4.166664568298827e-2), F(-1.388731625493765e-3), F(2.443315711809948e-5))
+
+
+def sincos(x):
+    k = np.floor(x * _TWO_OVER_PI + F(0.5))
+    r = ((x - k * _PIO2[0]) - k * _PIO2[1]) - k * _PIO2[2]
+    r2 = r * r
+    s = r + (r * r2) * (_SIN[0] + r2 * (_SIN[1] + r2 * _SIN[2]))
+    c = (F(1) - F(0.5) * r2) + (r2 * r2) * (_COS[0] + r2 * (_COS[1] + r2 * _COS[2]))
+    q = k.astype(np.int64) & 3
+    so = np.select([q == 0, q == 1, q == 2], [s, c, -s], -c)
+    co = np.select([q == 0, q == 1, q == 2], [c, -s, -c], s)
+    return so.astype(np.float32), co.astype(np.float32)
+
+
+def _lattice(ix, iy, iz, seed):
+    """Integer lattice hash -> [-1, 1): xor of per-axis multiplies, then a 32-bit finaliser."""
+    u = lambda a: a.astype(np.int64).astype(np.uint32)  # noqa: E731  two's complement wrap
+    h = np.uint32(seed) ^ (u(ix) * np.uint32(0x8da6b343)) ^ (u(iy) * np.uint32(0xd8163841)) ^ (u(iz) * np.uint32(0xcb1ab31f))
+    h = (h ^ (h >> np.uint32(16))) * np.uint32(0x7feb352d)
+    h = (h ^ (h >> np.uint32(15))) * np.uint32(0x846ca68b)
+    h = h ^ (h >> np.uint32(16))
+    return (h >> np.uint32(8)).astype(np.float32) * F(1.1920928955078125e-7) - F(1)
+
+
+def value_noise(x, y, z, seed):
+    """Trilinear value noise over the integer lattice with the smoothstep fade 3t^2 - 2t^3."""
+    fx0, fy0, fz0 = np.floor(x), np.floor(y), np.floor(z)
+    ix, iy, iz = fx0.astype(np.int64), fy0.astype(np.int64), fz0.astype(np.int64)
+    fx, fy, fz = x - fx0, y - fy0, z - fz0
+    ux, uy, uz = (fx * fx * (F(3) - F(2) * fx), fy * fy * (F(3) - F(2) * fy), fz * fz * (F(3) - F(2) * fz))
+    L = lambda a, b, c: _lattice(ix + a, iy + b, iz + c, seed)  # noqa: E731
+    lerp = lambda a, b, t: a + (b - a) * t  # noqa: E731
+    x00, x10 = lerp(L(0, 0, 0), L(1, 0, 0), ux), lerp(L(0, 1, 0), L(1, 1, 0), ux)
+    x01, x11 = lerp(L(0, 0, 1), L(1, 0, 1), ux), lerp(L(0, 1, 1), L(1, 1, 1), ux)
+    return lerp(lerp(x00, x10, uy), lerp(x01, x11, uy), uz)
+
+
+def deform(node, p):
+    """One deformer about its pivot c (DESIGN.md §6 'Deformers'): q = p - c, deform q, return q + c."""
+    op, ia, f = node.op, list(node.i), [F(v) for v in node.f]
+    q = [p[k] - f[k] for k in range(3)]
+    if op in (abi.SDF_TWIST, abi.SDF_BEND):
+        # rotate the plane perpendicular to `axis` by rate * q[axis] (twist) or amount * q[drive] (bend)
+        ax = ia[0]
+        drive = ax if op == abi.SDF_TWIST else ia[1]
+        u, w = (ax + 1) % 3, (ax + 2) % 3
+        s, c = sincos(f[3] * q[drive])
+        qu, qw = q[u], q[w]
+        q[u], q[w] = c * qu - s * qw, s * qu + c * qw
+    elif op == abi.SDF_TAPER:  # scale perpendicular to axis by 1 / lerp(start, end, t)
+        ax = ia[0]
+        u, w = (ax + 1) % 3, (ax + 2) % 3
+        t = _clamp((q[ax] + f[5] * F(0.5)) / f[5], F(0), F(1))
+        sc = f[3] + (f[4] - f[3]) * t
+        q[u], q[w] = q[u] / sc, q[w] / sc
+    elif op == abi.SDF_NOISE:  # q += amplitude * fbm3(frequency * q), `octaves`, `persistence`
+        octaves, seed = ia[0], ia[1]
+        x = [q[k] * f[3] for k in range(3)]
+        acc = []
+        for k in range(3):
+            amp, fr, tot = F(1), F(1), np.zeros_like(q[0])
+            for o in range(octaves):
+                sd = (seed + k * 0x9E3779B9 + o * 0x85EBCA6B) & 0xFFFFFFFF
+                tot = tot + amp * value_noise(x[0] * fr, x[1] * fr, x[2] * fr, sd)
+                amp = amp * f[5]
+                fr = fr * F(2)
+            acc.append(tot)
+        q = [q[k] + f[4] * acc[k] for k in range(3)]
+    elif op == abi.SDF_WAVE:  # q[disp] += amplitude * sin(frequency * q[axis])
+        ax, disp = ia[0], ia[1]
+        s, _ = sincos(f[4] * q[ax])
+        q[disp] = q[disp] + f[3] * s
+    else:
+        raise NotImplementedError(op)
+    return [q[k] + f[k] for k in range(3)]
+
+
+def sdf_eval(prog, p):
+    """The postfix program (include/rrte_hip.h): leaves push, CSG ops pop b, a and push op(a, b),
+    deformers save the point and replace it, POP_POINT restores it (d1.chain(d2) = d2(d1(p)))."""
+    vs, ps = [], []
+    for nd in prog:
+        op = nd.op
+        if op < 32:
+            vs.append(sdf_leaf(op, nd.f, p))
+        elif op < 64:
+            b, a = vs.pop(), vs.pop()
+            vs.append(csg(op, a, b, nd.f[0]))
+        elif op < 96:
+            ps.append(p)
+            p = deform(nd, p)
+        else:
+            p = ps.pop()
+    assert len(vs) == 1 and not ps
+    return vs[0]
+
+
+def sdf_march(pr, prog, o, d, tmin, tmax):
+    """SDFObject::intersect's search (README.md:458-467; DESIGN.md §6 'Sphere tracing'): march
+    inside the bounding sphere (p[0..3], |d| = 1) from max(t_min, t_enter) to min(t_max, t_exit);
+    hit when dist < eps * t, else t += dist * step_scale; a step past the end or max_steps = miss.
+    Vectorised: every ray steps while active.  Returns (hit mask, t)."""
+    n = o[0].shape[0]
+    c, br = [F(pr.p[k]) for k in range(3)], F(pr.p[3])
+    oc = [o[k] - c[k] for k in range(3)]
+    b = dot(oc, d)
+    cc = dot(oc, oc) - br * br
+    disc = b * b - cc
+    sq = np.sqrt(np.where(disc < F(0), F(0), disc))
+    lo, hi = -b - sq, -b + sq
+    tmin_a = np.broadcast_to(np.asarray(tmin, np.float32), (n,))
+    tmax_a = np.broadcast_to(np.asarray(tmax, np.float32), (n,))
+    t = np.where(lo > tmin_a, lo, tmin_a)      # max(t_min, t_enter), compare-select
+    tend = np.where(hi < tmax_a, hi, tmax_a)   # min(t_max, t_exit)
+    active = ~(disc < F(0)) & ~(t > tend)
+    hit = np.zeros(n, bool)
+    eps, scale = F(pr.sdf_hit_eps), F(pr.sdf_step_scale)
+    for _ in range(pr.sdf_max_steps):
+        if not active.any():
+            break
+        idx = np.nonzero(active)[0]
+        ti = t[idx]
+        dist = sdf_eval(prog, at([o[k][idx] for k in range(3)], [d[k][idx] for k in range(3)], ti))
+        h = dist < eps * ti
+        hit[idx[h]] = True
+        tn = ti + dist * scale
+        t[idx[~h]] = tn[~h]
+        active[idx[h | (tn > tend[idx])]] = False
+    return hit, t
+
+
+def sdf_attributes(prog, o, d, t):
+    """Hit point Ray::at(t) and the tetrahedral normal: taps at p + h k_i, h = 1e-3, k = (+,-,-),
+    (-,-,+), (-,+,-), (+,+,+), n = sum_i k_i f(p + h k_i) accumulated in that order, normalised."""
+    p = at(o, d, t)
+    hh = F(1e-3)
+    taps = [(1, -1, -1), (-1, -1, 1), (-1, 1, -1), (1, 1, 1)]
+    fs = [sdf_eval(prog, [p[k] + hh if s[k] > 0 else p[k] - hh for k in range(3)]) for s in taps]
+    n = [fs[0] if taps[0][k] > 0 else -fs[0] for k in range(3)]
+    for f_, s in zip(fs[1:], taps[1:]):
+        n = [n[k] + f_ if s[k] > 0 else n[k] - f_ for k in range(3)]
+    return p, normalize(n)

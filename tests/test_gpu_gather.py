@@ -83,6 +83,7 @@ def _check_gather(overlap, jit, batch, monkeypatch, alpha):
             p.flags |= abi.FLAG_GATHER_OVERLAP
         ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(p), 0, o.data_ptr(),
                                                     C.c_void_p(streams[i % 3].cuda_stream)))
+    ctx.check(lib.rrte_hip_flush(ctx.h))  # the partial batch's gather (collective)
     ctx.check(lib.rrte_hip_synchronize(ctx.h))
     for i, o in enumerate(outs):
         got = o.cpu().numpy().view(np.uint8)
@@ -140,6 +141,7 @@ def test_gather_batch_arguments_and_size_change(monkeypatch):
     for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
         ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
                                                     C.c_void_p(streams[i % 2].cuda_stream)))
+    ctx.check(lib.rrte_hip_flush(ctx.h))
     ctx.check(lib.rrte_hip_synchronize(ctx.h))
     for i, o in enumerate(outs):
         assert np.array_equal(o.cpu().numpy().view(np.uint8), want[i]), f"frame {i}"
@@ -178,6 +180,7 @@ def test_gather_batch_multi_frame_launches_and_changes(monkeypatch):
         for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
             ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
                                                         C.c_void_p(streams[i % 2].cuda_stream)))
+        ctx.check(lib.rrte_hip_flush(ctx.h))
         ctx.check(lib.rrte_hip_synchronize(ctx.h))
         for i, o in enumerate(outs):
             got = o.cpu().numpy().view(np.uint8)
