@@ -589,7 +589,7 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
 RRTE_UNROLL_(RRTE_MARCH_UNROLL)
         for (uint32_t i = 0; i < steps; ++i) {
             f3 p = ray_at(r, t);
-            float d = eval(p);
+            float d = eval_deferred(eval, p);
             hit = d < eps * t;
             const float tn = t + d * scale;
             const bool safe = (d - E * t >= D3) && ((d - dp) - E * (t - tp) >= D3);
@@ -605,7 +605,7 @@ RRTE_UNROLL_(RRTE_MARCH_UNROLL)
 RRTE_UNROLL_(RRTE_MARCH_UNROLL)
     for (uint32_t i = 0; i < steps; ++i) {
         f3 p = ray_at(r, t);
-        float d = eval(p);
+        float d = eval_deferred(eval, p);
         hit = d < eps * t;
         const float tn = t + d * scale;
         const bool stop = hit || tn > tend;
