@@ -23,8 +23,12 @@ import numpy as np
 # Frames in flight need their streams on distinct hardware queues.  HIP's default is 4 per process (the
 # GPU box exports GPU_MAX_HW_QUEUES=4), shared with torch's and the library's own streams; one rank of
 # an 8-GPU job then needs ~40 us for its share of a frame instead of ~24 us with 32 queues
-# (tools/r02_inflight.sh, 20 steps; the one-GPU frame is the same with 4 or 32).  Set before HIP starts.
-os.environ["GPU_MAX_HW_QUEUES"] = "32"
+# (tools/r02_inflight.sh, 20 steps; the one-GPU frame is the same with 4 or 32).  The bench's own
+# setting is RRTE_BENCH_HW_QUEUES (default 32), applied before HIP starts; the value in effect is
+# recorded in the JSON line (config.hw_queues).  Under rocprofv3 the profiler starts HIP before this
+# line runs, so the profiling scripts export GPU_MAX_HW_QUEUES themselves.
+HW_QUEUES = os.environ.get("RRTE_BENCH_HW_QUEUES", "32")
+os.environ["GPU_MAX_HW_QUEUES"] = HW_QUEUES
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -326,6 +330,31 @@ def main():
     torch.cuda.synchronize(dev)
     d2h_ms = e0.elapsed_time(e1)
 
+    # The drop-in boundary as Engine::render_frame uses it (engine.rs:280-312 -> raytracer.rs:45-89):
+    # blocking rrte_hip_render into a host RGBA8 buffer, D2H included -- into a reused buffer, and
+    # into a fresh zeroed buffer per frame as the reference allocates one (`vec![0u8; w*h*4]`,
+    # raytracer.rs:54).  Not the headline (SURVEY §8d excludes D2H); rank 0, N = 1 only.
+    boundary = None
+    if world == 1:
+        hbuf = np.zeros(W * H * 4, dtype=np.uint8)
+        pout = lambda b: b.ctypes.data_as(C.POINTER(C.c_uint8))  # noqa: E731
+        for _ in range(3):
+            ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), pout(hbuf)))
+        nb = 20
+        a = time.perf_counter()
+        for _ in range(nb):
+            ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), pout(hbuf)))
+        reused_ms = (time.perf_counter() - a) / nb * 1e3
+        a = time.perf_counter()
+        for _ in range(nb):
+            fresh = np.zeros(W * H * 4, dtype=np.uint8)
+            ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), pout(fresh)))
+        fresh_ms = (time.perf_counter() - a) / nb * 1e3
+        boundary = {"entry": "rrte_hip_render (blocking; Raytracer::render's signature, host RGBA8 out, D2H included)",
+                    "ms_per_frame_reused_buffer": round(reused_ms, 4),
+                    "ms_per_frame_fresh_buffer": round(fresh_ms, 4),
+                    "frames": nb, "note": "fresh = a new zeroed W*H*4 buffer per frame, as raytracer.rs:54 allocates"}
+
     # the reference's stock config on the generic kernel (rank 0, N=1 only; not the headline)
     stock = None
     if world == 1 and not args.no_stock:
@@ -378,6 +407,7 @@ def main():
                 "primary_rays_per_frame": W * H * prm.samples_per_pixel,
                 "shadow_rays_per_frame": shadow // args.steps,
                 "frames_in_flight": F,
+                "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "parallelism": f"rows{world}" if world > 1 else "single",
             },
             "roofline": {
@@ -408,6 +438,8 @@ def main():
                 line["valu"]["measured_peak"] = mp
                 line["valu"]["frac_of_measured_fma_class_peak"] = r / mp["fma_add_mul"]
                 line["valu"]["frac_of_measured_cmp_select_peak"] = r / mp["cmp_select_max"]
+        if boundary is not None:
+            line["boundary"] = boundary
         if stock is not None:
             line["stock_config"] = stock
         if world == 1 and not args.no_cpu:

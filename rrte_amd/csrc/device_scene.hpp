@@ -85,8 +85,9 @@ struct KParams {
     uint32_t num_prims, num_lights, num_materials;
     // row mapping: local row r -> image row (band interleave for multi-GPU)
     uint32_t rows;           // rows this launch renders
-    uint32_t band_rows;      // 0 = identity mapping
+    uint32_t band_rows;      // 0 = identity mapping (+ row0)
     uint32_t nranks, rank;
+    uint32_t row0;           // first image row of this launch (row-chunked blocking renders; band_rows == 0)
     float bg[4];
     float t_min, bias, inv_gamma, inv_spp;
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)

@@ -15,6 +15,7 @@ struct JitKernel {
     hipFunction_t fn = nullptr;
     double compile_ms = 0.0;
     size_t code_bytes = 0;
+    bool from_cache = false;
 };
 
 // HIP source for one scene + shading mode: the scene as static constexpr arrays
@@ -29,6 +30,7 @@ struct JitCode {
     std::vector<char> code;
     std::string log;
     double compile_ms = 0.0;
+    bool from_cache = false;  // loaded from the persistent code-object cache (jit.hip)
 };
 JitCode jit_compile_code(const std::string& src);  // compiles are serialised internally
 

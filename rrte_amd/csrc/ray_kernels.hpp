@@ -512,6 +512,53 @@ __device__ __forceinline__ float eval_deferred(const EVAL& eval, f3 p) {
 #endif
 }
 
+// The predicated sphere-tracing loop (RRTE_MARCH_PRED): the lanes of `live` (an SGPR lane mask) march
+// from t to tend under the caller's EXEC; a lane that has stopped keeps its state through selects on
+// that mask, the step counter is wave-uniform (SGPR), and the loop ends when no lane is left -- the
+// same t sequence and result per lane as the divergent-exit loops of sdf_march, without their per-step
+// EXEC save / restore chains on the scalar unit.
+template <class EVAL, bool CONVEX>
+__device__ __forceinline__ bool sdf_march_loop(const DPrim& pr, const EVAL& eval, const Ray& r, float t, float tend,
+                                               uint64_t live, float& t_hit) {
+    const f3 bc = V(pr.p[0], pr.p[1], pr.p[2]);
+    const float br = pr.p[3];
+    const float eps = pr.sdf_hit_eps, scale = pr.sdf_step_scale;
+    const uint32_t steps = pr.sdf_max_steps;
+    [[maybe_unused]] float E = 0.0f, D3 = 0.0f, dp = __builtin_nanf(""), tp = t;
+    if constexpr (CONVEX) {
+        E = eps * (1.0f + 0x1p-20f);
+        constexpr float K = EVAL::kLeafScale;
+        D3 = 3.0f * 0x1p-17f *
+             ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
+              ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
+    }
+    // every condition as a wave mask (one v_cmp each, combined on the scalar unit)
+    uint64_t hitm = 0ull;
+    uint32_t left = steps;
+    if (left != 0u) {
+        for (;;) {
+            const f3 p = ray_at(r, t);
+            const float d = eval_deferred(eval, p);
+            const float tn = t + d * scale;
+            const uint64_t hm = __builtin_amdgcn_ballot_w64(d < eps * t);
+            uint64_t sm = hm | __builtin_amdgcn_ballot_w64(tn > tend);
+            if constexpr (CONVEX) {
+                sm |= __builtin_amdgcn_ballot_w64(d - E * t >= D3) &
+                      __builtin_amdgcn_ballot_w64((d - dp) - E * (t - tp) >= D3);
+                dp = d;
+                tp = t;
+            }
+            hitm |= hm & live;
+            t = mask_select(live & ~hm, t, tn);
+            live &= ~sm;
+            left = __builtin_amdgcn_readfirstlane(left - 1u);
+            if ((left == 0u) | (live == 0ull)) break;
+        }
+    }
+    t_hit = t;
+    return mask_lane(hitm);
+}
+
 template <class EVAL, bool ANY = false, bool CONVEX = false>
 __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, const Ray& r, float t_min, float t_max,
                                           float& t_hit) {
@@ -520,6 +567,25 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     f3 oc = vsub(r.o, bc);
     float b = vdot(oc, r.d);
     float cc = vdot(oc, oc) - br * br;
+#if RRTE_MARCH_PRED
+    // Predicated bound test: no divergent early return -- every lane of the caller's EXEC computes the
+    // entry and exit parameters, `enter` says whether it marches (the same decisions as the branches
+    // below), and the march loop runs under the caller's EXEC with the marching lanes in `live`.
+    // Lanes that do not enter get a benign t (their points stay finite, so no guard fallback runs).
+    {
+        const float disc = b * b - cc;
+        bool enter = !(disc < 0.0f);
+        if constexpr (ANY) enter = enter & !(t_max == t_max && leaves_sphere(b, cc, 1.0f, t_min));
+        const float sq = sqrt_rn(disc < 0.0f ? 1.0f : disc);
+        float t = mx(t_min, -b - sq);
+        const float tend = mn(t_max, -b + sq);
+        enter = enter & !(t > tend);
+        uint64_t live = __builtin_amdgcn_ballot_w64(enter);
+        if (live == 0ull) return false;
+        t = enter ? t : 1.0f;
+        return sdf_march_loop<EVAL, CONVEX>(pr, eval, r, t, tend, live, t_hit);
+    }
+#endif
     // the bound test below has no divide (roots -b -/+ sq): leaves_sphere's argument with a = 1, which
     // leaves tend = mn(t_max, -b + sq) <= 2^-60 < t_min <= t unless t_max is NaN (tend NaN marches on)
     if (ANY && t_max == t_max && leaves_sphere(b, cc, 1.0f, t_min)) return false;
@@ -535,50 +601,6 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     // t sequence and result as "if (d < eps*t) hit; t += d*scale; if (t > tend) miss" (NaN
     // included).  (A fully predicated form with a wave-uniform exit was measured slower.)
     bool hit = false;
-#if RRTE_MARCH_PRED
-    // Predicated march: the lanes that get here step together under one EXEC mask.  `live` (an SGPR
-    // lane mask) holds the lanes still marching; a lane that has stopped keeps its state through
-    // selects on that mask, the step counter is wave-uniform (SGPR), and the loop ends when no lane
-    // is left -- the same t sequence and result per lane as the divergent-exit loops below, without
-    // their per-step EXEC save / restore chains on the scalar unit.
-    {
-        uint64_t live = __builtin_amdgcn_ballot_w64(true);
-        [[maybe_unused]] float E = 0.0f, D3 = 0.0f, dp = __builtin_nanf(""), tp = t;
-        if constexpr (CONVEX) {
-            E = eps * (1.0f + 0x1p-20f);
-            constexpr float K = EVAL::kLeafScale;
-            D3 = 3.0f * 0x1p-17f *
-                 ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
-                  ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
-        }
-        // every condition as a wave mask (one v_cmp each, combined on the scalar unit)
-        uint64_t hitm = 0ull;
-        uint32_t left = steps;
-        if (left != 0u) {
-            for (;;) {
-                const f3 p = ray_at(r, t);
-                float d = eval_deferred(eval, p);
-                const float tn = t + d * scale;
-                const uint64_t hm = __builtin_amdgcn_ballot_w64(d < eps * t);
-                uint64_t sm = hm | __builtin_amdgcn_ballot_w64(tn > tend);
-                if constexpr (CONVEX) {
-                    sm |= __builtin_amdgcn_ballot_w64(d - E * t >= D3) &
-                          __builtin_amdgcn_ballot_w64((d - dp) - E * (t - tp) >= D3);
-                    dp = d;
-                    tp = t;
-                }
-                hitm |= hm & live;
-                t = mask_select(live & ~hm, t, tn);
-                live &= ~sm;
-                left = __builtin_amdgcn_readfirstlane(left - 1u);
-                if ((left == 0u) | (live == 0ull)) break;
-            }
-        }
-        hit = mask_lane(hitm);
-        t_hit = t;
-        return hit;
-    }
-#endif
     if constexpr (CONVEX) {
         const float E = eps * (1.0f + 0x1p-20f);
         constexpr float K = EVAL::kLeafScale;
@@ -1207,8 +1229,18 @@ __device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min,
         // one wave-uniform skip test: culled, or every lane already occluded (mask cleared)
         if (mask == 0 || (i < 64u && !((mask >> i) & 1ull))) return;
         Hit h;
+#if RRTE_MARCH_PRED
+        // predicated: every lane of the caller's EXEC runs the test (marches stay wide, see
+        // sdf_march_loop); lanes that are already occluded or that cast no ray (t_max = -inf) get an
+        // empty interval, for which every intersector reports no hit
+        const float tm = (hit_any || (int)i == self) ? -kInf : t_max;
+        const bool hi = any_hit_at(sc, ii, r, t_min, tm, h);
+        hit_any = hit_any | hi;
+        if (__all(hit_any | !(t_max != -kInf))) mask = 0;
+#else
         if (!hit_any && (int)i != self && any_hit_at(sc, ii, r, t_min, t_max, h)) hit_any = true;
         if (__all(hit_any)) mask = 0;
+#endif
     });
     return hit_any;
 }
@@ -1626,12 +1658,18 @@ __device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray
 // LAMBERT_SHADOW (build-defined) for one camera ray.  Called by
 // all 64 lanes of the wave (`live` marks the lanes that own a pixel): with
 // CULL the hit-point bound and the per-light shadow culls are wave reductions.
+constexpr bool kShadeAll = RRTE_MARCH_PRED != 0;  // shade every lane (predicated), or only hit lanes
 template <class S, bool CULL>
 __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, const Cull& cl, const Ray& r, bool live,
                                              uint32_t& nshadow, uint32_t pmask = ~0u) {
     Col out{0.0f, 0.0f, 0.0f, 1.0f};
     if (kp.max_depth == 0) return out;
     Hit h;
+    h.t = 0.0f;  // lanes without a hit keep a benign point and normal (predicated shading, RRTE_MARCH_PRED)
+    h.p = V(0.0f, 0.0f, 0.0f);
+    h.n = V(0.0f, 1.0f, 0.0f);
+    h.front = true;
+    h.sub = 0u;
     // RRTE_DEBUG bit 7 (timing diagnostics only, with bit 1): the closest-hit search without hit attributes
     const int idx = closest_hit(sc, r, live ? kp.t_min : kInf, h, pmask, !(kp.debug & 128u));  // idle lanes find nothing
     const DMaterial* m = idx >= 0 ? material_of(sc, idx) : nullptr;
@@ -1656,13 +1694,34 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
     auto shade = [&](const DLight& l, uint64_t smask, uint32_t li) {
         Contrib k = illuminate(l, h.p);
         if (l.kind == RRTE_LIGHT_AMBIENT) {
-            cr = cr + ar * k.cr;
-            cg = cg + ag * k.cg;
-            cb = cb + ab * k.cb;
+            if (hit) {
+                cr = cr + ar * k.cr;
+                cg = cg + ag * k.cg;
+                cb = cb + ab * k.cb;
+            }
             return;
         }
         const float ndl = vdot(h.n, k.dir);
+#if RRTE_MARCH_PRED
+        // predicated over every lane (hit or not): a lane that casts no shadow ray tests the empty
+        // interval (t_max = -inf) along a benign direction, so the any-hit marches run wide
+        const bool cast = hit && ndl > 0.0f && k.att > 0.0f;
+        nshadow += cast ? 1u : 0u;
+        {
+            const Ray sr = ray_new_unit(vadd(h.p, vmuls(h.n, bias)), cast ? k.dir : V(0.0f, 1.0f, 0.0f));
+            const bool skip = (kp.debug & 1u) || ((kp.debug & 256u) && li != ((kp.debug >> 9) & 7u));
+            const bool occ = !skip && occluded(sc, sr, bias, cast ? k.dist : -kInf, smask, (kp.debug & 64u) ? idx : -1);
+            if (cast && !occ) {
+                float f = k.att * ndl;
+                cr = cr + ar * (k.cr * f);
+                cg = cg + ag * (k.cg * f);
+                cb = cb + ab * (k.cb * f);
+            }
+        }
+        if (false) {
+#else
         if (ndl > 0.0f && k.att > 0.0f) {
+#endif
             ++nshadow;
             Ray sr = ray_new_unit(vadd(h.p, vmuls(h.n, bias)), k.dir);
             // RRTE_DEBUG bit 6 (timing diagnostics only, wrong images): skip the object the ray starts on
@@ -1676,7 +1735,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
         }
     };
     if constexpr (!CULL) {
-        if (hit) for_each_light(sc, [&](auto lii) { shade(light_at(sc, lii), ~0ull, (uint32_t)lii); });
+        if (kShadeAll || hit) for_each_light(sc, [&](auto lii) { shade(light_at(sc, lii), ~0ull, (uint32_t)lii); });
     } else {
         HitBound hb{};
         hb.unsafe = true;  // no bounds table: every mask all-ones
@@ -1691,14 +1750,14 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
                 auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii), bnd); };
                 static_for<0, S::num_lights>(cull_one);
             }
-            auto shade_one = [&](auto lii) { if (hit) shade(light_at(sc, lii), smask[(uint32_t)lii], (uint32_t)lii); };
+            auto shade_one = [&](auto lii) { if (kShadeAll || hit) shade(light_at(sc, lii), smask[(uint32_t)lii], (uint32_t)lii); };
             static_for<0, S::num_lights>(shade_one);
         } else {
             const float4 bnd = cull_on(cl) ? load_bound(cl) : float4{};
 #pragma unroll 1
             for (uint32_t li = 0; li < sc.num_lights; ++li) {
                 const uint64_t sm = shadow_cull(cl, hb, sc.lights[li], bnd);
-                if (hit) shade(sc.lights[li], sm, li);
+                if (kShadeAll || hit) shade(sc.lights[li], sm, li);
             }
         }
     }
@@ -1740,7 +1799,7 @@ __device__ __forceinline__ uint32_t gamma22_u8(float c) {
 
 // Map this launch's local row to the image row (band interleave, §8e).
 __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
-    if (kp.band_rows == 0) return r;
+    if (kp.band_rows == 0) return r + kp.row0;
     uint32_t b = r / kp.band_rows, w = r - b * kp.band_rows;
     return (b * kp.nranks + kp.rank) * kp.band_rows + w;
 }

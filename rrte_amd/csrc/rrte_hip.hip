@@ -19,6 +19,9 @@
 #include <cstring>
 #include <future>
 #include <thread>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -127,6 +130,31 @@ struct rrte_ctx {
     uint64_t fault_stall_at = 0;
     uint32_t* h_stall = nullptr;       // pinned, device-visible release flag
     bool stall_armed = false;
+    // Blocking drop-in path (rrte_hip_render into a host buffer, Raytracer::render's signature): the
+    // frame renders into HBM, a blit kernel moves it in kHostChunks row chunks into pinned host
+    // memory mapped to the device (wide stores over PCIe: ~52 GB/s against ~30 GB/s for an SDMA copy
+    // to pinned memory and ~22 GB/s to pageable memory, tools/micro/d2h.hip), and host threads copy
+    // each chunk into the caller's buffer as soon as its event has fired.  RRTE_BOUNDARY_PIPE=0: the
+    // plain pageable hipMemcpy (A/B).
+    static constexpr int kHostChunks = 8, kCopyHelpers = 2;
+    bool boundary_pipe = true;
+    uint8_t* h_stage = nullptr;        // pinned, mapped
+    uint8_t* d_stage = nullptr;        // its device address
+    size_t cap_stage = 0;
+    hipEvent_t ev_chunk[kHostChunks] = {};
+    struct CopyJob {
+        std::mutex mu;
+        std::condition_variable cv;
+        uint64_t gen = 0;              // bumped per frame (helpers wake up)
+        bool quit = false;
+        std::atomic<int> pending{0};   // helpers still copying this frame
+        uint8_t* dst = nullptr;
+        const uint8_t* src = nullptr;
+        size_t chunk_bytes[kHostChunks] = {}, chunk_off[kHostChunks] = {};
+        int nchunks = 0;
+        const hipEvent_t* ev = nullptr;
+    } job;
+    std::vector<std::thread> helpers;
     rrte_stats stats{};
     bool pending_kernel_timing = false;
     uint64_t pending_primary = 0;
@@ -888,6 +916,86 @@ rrte_status finish_frame(rrte_ctx* c) {
     return RRTE_OK;
 }
 
+// Wide device -> host copy of one chunk: 16-byte stores, consecutive lanes consecutive addresses.
+__global__ __launch_bounds__(256) void blit_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, size_t bytes) {
+    const size_t n16 = bytes / 16u;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    if (blockIdx.x == 0 && threadIdx.x < (bytes & 15u)) dst[n16 * 16u + threadIdx.x] = src[n16 * 16u + threadIdx.x];
+}
+
+// One thread's share of the host copies: slice `part` of `parts` of every chunk, each chunk as soon as
+// its blit has landed (events polled; hipEventQuery is thread-safe).
+static void copy_share(rrte_ctx::CopyJob& j, int part, int parts) {
+    for (int k = 0; k < j.nchunks; ++k) {
+        while (hipEventQuery(j.ev[k]) == hipErrorNotReady) std::this_thread::yield();
+        const size_t n = j.chunk_bytes[k], per = (n / parts + 63) & ~(size_t)63;
+        const size_t a = std::min(n, per * part), b = std::min(n, a + per);
+        if (b > a) memcpy(j.dst + j.chunk_off[k] + a, j.src + j.chunk_off[k] + a, b - a);
+    }
+}
+
+static void copy_helper(rrte_ctx* c, int idx) {
+    rrte_ctx::CopyJob& j = c->job;
+    uint64_t seen = 0;
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(j.mu);
+            j.cv.wait(lk, [&] { return j.quit || j.gen != seen; });
+            if (j.quit) return;
+            seen = j.gen;
+        }
+        copy_share(j, idx + 1, rrte_ctx::kCopyHelpers + 1);
+        j.pending.fetch_sub(1, std::memory_order_acq_rel);
+    }
+}
+
+// The blocking path's D2H (see rrte_ctx::boundary_pipe): blits into the pinned stage chunk by chunk on
+// the context stream after the render, host threads copy each chunk out as it lands.
+static rrte_status host_copy_pipelined(rrte_ctx* c, uint8_t* out, size_t bytes) {
+    if (c->cap_stage < bytes) {
+        if (c->h_stage) HIPCHK(c, hipHostFree(c->h_stage));
+        c->h_stage = nullptr;
+        c->cap_stage = 0;
+        HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), bytes, hipHostMallocMapped));
+        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_stage), c->h_stage, 0));
+        c->cap_stage = bytes;
+    }
+    if (!c->ev_chunk[0])
+        for (hipEvent_t& e : c->ev_chunk) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (c->helpers.empty())
+        for (int i = 0; i < rrte_ctx::kCopyHelpers; ++i) c->helpers.emplace_back(copy_helper, c, i);
+    rrte_ctx::CopyJob& j = c->job;
+    const int nch = bytes >= (1u << 20) ? rrte_ctx::kHostChunks : 1;
+    const size_t per = ((bytes + nch - 1) / nch + 255) & ~(size_t)255;
+    j.nchunks = 0;
+    for (int k = 0; k < nch; ++k) {
+        const size_t a = std::min(bytes, per * k), b = std::min(bytes, a + per);
+        if (b <= a) break;
+        const uint32_t blocks = (uint32_t)std::min<size_t>(1024, ((b - a) / 16 + 255) / 256 + 1);
+        hipLaunchKernelGGL(blit_kernel, dim3(blocks), dim3(256), 0, c->stream,
+                           reinterpret_cast<const uint8_t*>(c->d_rgba) + a, c->d_stage + a, b - a);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->ev_chunk[k], c->stream));
+        j.chunk_off[k] = a;
+        j.chunk_bytes[k] = b - a;
+        ++j.nchunks;
+    }
+    j.dst = out;
+    j.src = c->h_stage;
+    j.ev = c->ev_chunk;
+    j.pending.store(rrte_ctx::kCopyHelpers, std::memory_order_release);
+    {
+        std::lock_guard<std::mutex> lk(j.mu);
+        ++j.gen;
+    }
+    j.cv.notify_all();
+    copy_share(j, 0, rrte_ctx::kCopyHelpers + 1);
+    while (j.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    return RRTE_OK;
+}
+
 rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out8,
                           float* outf) {
     rrte_status r = validate(c, s, p);
@@ -912,8 +1020,12 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     c->pending_primary = (uint64_t)npix * p->samples_per_pixel;
     c->stats.upload_ms = up;
     c->stats.gather_ms = 0.0;
-    if (out8) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
-    if (outf) HIPCHK(c, hipMemcpyAsync(outf, c->d_f32, npix * 16, hipMemcpyDeviceToHost, c->stream));
+    if (out8 && !outf && c->boundary_pipe) {
+        if ((r = host_copy_pipelined(c, out8, npix * 4)) != RRTE_OK) return r;
+    } else {
+        if (out8) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
+        if (outf) HIPCHK(c, hipMemcpyAsync(outf, c->d_f32, npix * 16, hipMemcpyDeviceToHost, c->stream));
+    }
     if ((r = finish_frame(c)) != RRTE_OK) return r;
     c->stats.frames++;
     return RRTE_OK;
@@ -977,6 +1089,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_DIAG_SKIP")) c->env_diag_skip = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GATHER_RGB24")) c->env_gather_rgba = g[0] == '0';
     c->env_guard_leaves = env_guard_setting();
+    if (const char* g = getenv("RRTE_BOUNDARY_PIPE")) c->boundary_pipe = g[0] != '0';
     if (const char* g = getenv("RRTE_COMM_TIMEOUT_MS")) c->comm_timeout_ms = std::max<uint32_t>(1u, (uint32_t)strtoul(g, nullptr, 0));
     if (const char* g = getenv("RRTE_FAULT_STALL_GATHER")) c->fault_stall_at = strtoull(g, nullptr, 0);
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
@@ -1035,6 +1148,15 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_stall) (void)hipHostFree(c->h_stall);
+    {
+        std::lock_guard<std::mutex> lk(c->job.mu);
+        c->job.quit = true;
+    }
+    c->job.cv.notify_all();
+    for (auto& t : c->helpers) t.join();
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    for (hipEvent_t e : c->ev_chunk)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_poll)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1499,6 +1621,8 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
     // bytes per rank slot, 256-B aligned so every rank's send buffer starts aligned
     const size_t slice = ((size_t)cap * p->width * (rgb24 ? 3u : 4u) + 255u) & ~(size_t)255u;
     const uint32_t kflags = rgb24 ? kFlagSlabRgb24 : 0u;
+    if (c->comm_failed)
+        return fail(c, RRTE_RCCL_ERROR, "communicator aborted earlier (%s); call rrte_hip_comm_init", c->comm_fail_msg.c_str());
     // one rank: no exchange (RRTE_FORCE_GATHER=1 still takes the gather path: tests on one GPU)
     if (c->nranks == 1 && !(c->env_force_gather && c->comm)) {
         r = launch(c, s, p, p->height, static_cast<uint32_t*>(d_full), nullptr, st);
@@ -1506,7 +1630,6 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         if (timing) HIPCHK(c, hipEventRecord(c->ev1, st));
         return r;
     }
-    if (c->comm_failed) return fail(c, RRTE_RCCL_ERROR, "communicator aborted earlier (%s); call rrte_hip_comm_init", c->comm_fail_msg.c_str());
     if (!c->comm) return fail(c, RRTE_INVALID_ARG, "rrte_hip_comm_init has not been called");
     if (c->gather_batch > 1 && !timing) {
         rrte_ctx::Batch& b = c->batch;

@@ -423,3 +423,23 @@ def test_invalid_inputs_fail_loudly():
     assert ctx.lib.rrte_hip_render(ctx.h, bad2.ref(), C.byref(cfg.lower()), out.ctypes.data) == abi.RRTE_UNSUPPORTED_PRIM
     h = C.c_void_p()
     assert ctx.lib.rrte_hip_create(99, C.byref(h)) == abi.RRTE_NO_DEVICE
+
+
+def test_jit_code_objects_persist_across_contexts(tmp_path, monkeypatch):
+    """The persistent code-object cache (jit.hip): a second context specialising the same scene loads
+    the compiled kernel from RRTE_JIT_CACHE_DIR instead of running hiprtc again, and renders the same
+    bytes; a different scene misses the cache."""
+    monkeypatch.setenv("RRTE_JIT_CACHE_DIR", str(tmp_path))
+    objs, lights, cam, cfg = scenes.sdf_showcase(96, 54)
+    a = Raytracer(cfg, device=0, jit=abi.JIT_ON)
+    img_a = a.render(objs, lights, [], cam)
+    cold = a.stats().jit_compile_ms
+    assert a.stats().jit_active == 1 and len(list(tmp_path.glob("*.hsaco"))) == 1
+    b = Raytracer(cfg, device=0, jit=abi.JIT_ON)
+    img_b = b.render(objs, lights, [], cam)
+    warm = b.stats().jit_compile_ms
+    assert b.stats().jit_active == 1 and np.array_equal(img_a, img_b)
+    assert warm < 0.2 * cold, (cold, warm)
+    lights[0].intensity = np.float32(lights[0].intensity * 0.5)  # another scene: another kernel
+    b.render(objs, lights, [], cam)
+    assert len(list(tmp_path.glob("*.hsaco"))) == 2
