@@ -164,6 +164,44 @@ def measured_valu_peak():
     return {"fma_add_mul": fma, "cmp_select_max": sel, "source": "profiles/r01_valu_peak.json"}
 
 
+def kernel_variants(scene, prm, fulls, sptrs, dev, rays_per_frame, n=60):
+    """Secondary throughput of the headline workload per kernel kind (rank 0, N=1; not the headline):
+    the generic kernel, the TOPOLOGY specialisation (structure compiled in, values read from the
+    uploaded scene: one compile serves every frame of an animation) and the FULL specialisation (the
+    headline's kernel), each on a context of its own, frames in flight as the headline runs them."""
+    import torch
+    out = {}
+    F = len(fulls)
+    for kind, jit, topo in (("generic", abi.JIT_OFF, "0"), ("topology", abi.JIT_ON, "1"), ("full", abi.JIT_ON, "0")):
+        old = os.environ.get("RRTE_JIT_TOPO")
+        os.environ["RRTE_JIT_TOPO"] = topo  # read at context creation
+        try:
+            c = Context(dev.index, jit=jit)
+        finally:
+            if old is None:
+                os.environ.pop("RRTE_JIT_TOPO", None)
+            else:
+                os.environ["RRTE_JIT_TOPO"] = old
+        go = lambda i: c.check(c.lib.rrte_hip_render_async(c.h, scene.ref(), C.byref(prm),  # noqa: E731
+                                                           fulls[i % F].data_ptr(), None, sptrs[i % F]))
+        for i in range(F + 1):
+            go(i)
+        torch.cuda.synchronize(dev)
+        a = time.perf_counter()
+        for i in range(n):
+            go(i)
+        torch.cuda.synchronize(dev)
+        ts = (time.perf_counter() - a) / n
+        st = c.stats()
+        out[kind] = {"value": round(rays_per_frame / ts / 1e6, 3), "unit": "Mray/s", "ms_per_frame": round(ts * 1e3, 4),
+                     "jit_active": int(st.jit_active)}
+        c.check(c.lib.rrte_hip_synchronize(c.h))
+        c.close()
+    out["note"] = (f"{n} frames each, {F} in flight; jit_active 0 generic / 1 full / 2 topology "
+                   "(include/rrte_hip.h rrte_hip_set_jit)")
+    return out
+
+
 def stock_config(args):
     """The reference's own default workload on the same scene (SURVEY §8d secondary number):
     REFCOMPAT, spp 4, max_depth 50, random jitter and scatter (counter-based RNG)."""
@@ -355,6 +393,10 @@ def main():
                     "ms_per_frame_fresh_buffer": round(fresh_ms, 4),
                     "frames": nb, "note": "fresh = a new zeroed W*H*4 buffer per frame, as raytracer.rs:54 allocates"}
 
+    kinds = None
+    if world == 1 and not args.no_stock:
+        kinds = kernel_variants(scene, prm, fulls, sptrs, dev, W * H * prm.samples_per_pixel + shadow // args.steps)
+
     # the reference's stock config on the generic kernel (rank 0, N=1 only; not the headline)
     stock = None
     if world == 1 and not args.no_stock:
@@ -438,8 +480,19 @@ def main():
                 line["valu"]["measured_peak"] = mp
                 line["valu"]["frac_of_measured_fma_class_peak"] = r / mp["fma_add_mul"]
                 line["valu"]["frac_of_measured_cmp_select_peak"] = r / mp["cmp_select_max"]
+            # the same instructions issued at the frame rate of the timed stream (frames in flight): the
+            # lone-launch rate above includes one frame's fill and drain, the stream rate does not
+            insts = pmc.get("counters_per_dispatch", {}).get("SQ_INSTS_VALU")
+            if insts:
+                fr = insts / (elapsed / args.steps)
+                line["valu"]["wave_instr_per_s_at_frame_rate"] = fr
+                line["valu"]["issue_frac_at_frame_rate"] = fr / line["valu"]["peak_wave_instr_per_s"]
+                if mp:
+                    line["valu"]["frac_of_measured_fma_class_peak_at_frame_rate"] = fr / mp["fma_add_mul"]
         if boundary is not None:
             line["boundary"] = boundary
+        if kinds is not None:
+            line["kernel_kinds"] = kinds
         if stock is not None:
             line["stock_config"] = stock
         if world == 1 and not args.no_cpu:

@@ -262,7 +262,7 @@ typedef struct rrte_stats {
     double gather_ms;        /* RCCL gather + de-interleave time               */
     double upload_ms;        /* scene H2D time (0 when the scene was cached)   */
     uint64_t frames;         /* frames rendered by this context                */
-    uint32_t jit_active;     /* 1 if the last frame ran a scene-specialised kernel */
+    uint32_t jit_active;     /* last frame's kernel: 0 generic, 1 full, 2 topology specialisation */
     uint32_t _pad0;
     double jit_compile_ms;   /* hiprtc compile time of the last specialised kernel */
 } rrte_stats;
@@ -306,11 +306,19 @@ rrte_status rrte_hip_stats(rrte_ctx* ctx, rrte_stats* out);
 /* Scene-specialised kernels (hiprtc).  OFF: always the
  * generic kernel.  ON: specialise a scene on its first frame.  AUTO (default):
  * specialise once the same scene is rendered a second time.  Results are
- * bit-identical either way; env RRTE_JIT=0/1/2 overrides the default. */
+ * bit-identical either way; env RRTE_JIT=0/1/2 overrides the default.
+ * A specialisation is FULL (every scene value compiled in) or TOPOLOGY (object kinds, SDF
+ * programs' ops and structure, light kinds compiled in; positions, sizes, colours, intensities
+ * read from the uploaded scene), so moving, resizing or recolouring objects and lights reuses one
+ * compiled kernel.  Which: env RRTE_JIT_TOPO=0 full only, =1 topology only, unset/2 adaptive --
+ * topology once a scene change kept the previous scene's topology (an animation), full once a
+ * scene has been rendered unchanged for 16 frames.  Compiled code objects persist on disk
+ * (RRTE_JIT_CACHE_DIR, default $XDG_CACHE_HOME/rrte-jit or ~/.cache/rrte-jit; RRTE_JIT_CACHE=0 off). */
 typedef enum rrte_jit_mode { RRTE_JIT_OFF = 0, RRTE_JIT_ON = 1, RRTE_JIT_AUTO = 2 } rrte_jit_mode;
 rrte_status rrte_hip_set_jit(rrte_ctx* ctx, int mode);
-/* Diagnostic: generate + hiprtc-compile the specialised kernel for `scene`
- * (no device needed).  RRTE_OK if it compiles; otherwise the log is copied out. */
+/* Diagnostic: generate + hiprtc-compile the specialised kernel for `scene` (the full one; the
+ * topology one with env RRTE_JIT_TOPO=1) -- no device needed.  RRTE_OK if it compiles; otherwise
+ * the log is copied out. */
 rrte_status rrte_hip_jit_check(const rrte_scene_ir* scene, int mode, char* log, size_t log_len);
 /* Diagnostic: run the kernels' short correctly rounded f32 sequences (device_scene.hpp
  * sqrt_rn / rcp_rn / the constant-divisor step of div_rn) on `device` against the

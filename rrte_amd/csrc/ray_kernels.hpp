@@ -37,6 +37,7 @@ struct MeshView {
 
 struct SceneView {
     static constexpr bool kStatic = false;
+    static constexpr bool kTopo = false;
     const DPrim* __restrict__ prims;
     const DMaterial* __restrict__ mats;
     const DLight* __restrict__ lights;
@@ -84,23 +85,77 @@ __device__ __forceinline__ void for_each_prim_exp(const S& sc, F&& f) {
     if constexpr (S::kStatic && (RRTE_EXP_PRIM_ORDER & BIT)) static_for_rev<0, S::num_prims>(f);
     else for_each_prim(sc, f);
 }
-// Scene record accessors.  For a static scene the record is copied in a
-// constant-expression context (constexpr local): device-side copies of
+// Scene-specialised kernels come in two kinds (jit.hip).  FULL (S::kTopo false): every scene record
+// is a static constexpr array, so all scene constants fold into the code.  TOPOLOGY (S::kTopo true):
+// only the scene's structure is compile-time -- object kinds, materials and SDF node ranges, node
+// ops, integer arguments and CSG-guard links, light kinds, the convexity and cullability decisions
+// (TopoPrim / TopoNode / TopoLight) -- while positions, sizes, matrices, colours and intensities are
+// read from the uploaded scene records with wave-uniform (scalar) loads, so moving or recolouring an
+// object needs no recompile.  The accessors below give both kinds the same interface.
+struct TopoPrim { uint32_t kind; uint32_t sdf_first, sdf_count; bool convex; };
+struct TopoNode { uint32_t op; uint32_t i[3]; };
+struct TopoLight { uint32_t kind; bool cullable; };
+// The uploaded records a topology kernel reads (a kernel argument).
+struct SceneValues {
+    const DPrim* prims;
+    const DMaterial* mats;
+    const DLight* lights;
+    const rrte_sdf_node* nodes;
+};
+
+// Scene record accessors.  For a full static scene the record is copied in a
+// constexpr-expression context (constexpr local): device-side copies of
 // constexpr globals may be emitted as externally-initialised memory whose
-// loads do not fold, while a constexpr copy always does.
+// loads do not fold, while a constexpr copy always does.  For a topology scene
+// the record is loaded and its structural fields replaced by their compile-time values.
 template <class S>
 __device__ __forceinline__ const DPrim& prim_at(const S& sc, uint32_t i) { return sc.prims[i]; }
 template <class S, uint32_t I>
-__device__ __forceinline__ DPrim prim_at(const S&, UC<I>) {
-    constexpr DPrim v = S::prims[I];
-    return v;
+constexpr uint32_t prim_kind() {
+    if constexpr (S::kTopo) return S::topo_prims[I].kind;
+    else return S::prims[I].kind;
+}
+template <class S, uint32_t I>
+constexpr uint32_t prim_first() {
+    if constexpr (S::kTopo) return S::topo_prims[I].sdf_first;
+    else return S::prims[I].sdf_first;
+}
+template <class S, uint32_t I>
+constexpr uint32_t prim_count() {
+    if constexpr (S::kTopo) return S::topo_prims[I].sdf_count;
+    else return S::prims[I].sdf_count;
+}
+template <class S, uint32_t I>
+__device__ __forceinline__ DPrim prim_at(const S& sc, UC<I>) {
+    if constexpr (S::kTopo) {
+        constexpr TopoPrim tp = S::topo_prims[I];
+        DPrim v = sc.prims[I];
+        v.kind = tp.kind;
+        v.sdf_first = tp.sdf_first;
+        v.sdf_count = tp.sdf_count;
+        return v;
+    } else {
+        constexpr DPrim v = S::prims[I];
+        return v;
+    }
 }
 template <class S>
 __device__ __forceinline__ const DLight& light_at(const S& sc, uint32_t i) { return sc.lights[i]; }
 template <class S, uint32_t I>
-__device__ __forceinline__ DLight light_at(const S&, UC<I>) {
-    constexpr DLight v = S::lights[I];
-    return v;
+constexpr uint32_t light_kind() {
+    if constexpr (S::kTopo) return S::topo_lights[I].kind;
+    else return S::lights[I].kind;
+}
+template <class S, uint32_t I>
+__device__ __forceinline__ DLight light_at(const S& sc, UC<I>) {
+    if constexpr (S::kTopo) {
+        DLight v = sc.lights[I];
+        v.kind = light_kind<S, I>();
+        return v;
+    } else {
+        constexpr DLight v = S::lights[I];
+        return v;
+    }
 }
 
 template <class S, class F>
@@ -257,16 +312,17 @@ __device__ __forceinline__ f3 sdf_deform(G& g, uint32_t op, const uint32_t* __re
 // One postfix node applied to the value / point stacks (leaves push a
 // distance, CSG ops pop two and push one, deformers push the point and
 // replace it, POP_POINT restores it).
+// (op and the integer arguments separately from the float arguments: a topology kernel has the
+// first two at compile time and reads the third.)
 template <class G>
-__device__ __forceinline__ void sdf_node_step(G& g, const rrte_sdf_node& n, float* vs, f3* ps, uint32_t& sp, uint32_t& pp,
-                                              f3& p) {
-    const uint32_t op = n.op;
+__device__ __forceinline__ void sdf_node_step(G& g, uint32_t op, const uint32_t* iargs, const float* fargs, float* vs,
+                                              f3* ps, uint32_t& sp, uint32_t& pp, f3& p) {
     if (op < 32) {
-        vs[sp] = sdf_leaf(g, op, n.f, p);
+        vs[sp] = sdf_leaf(g, op, fargs, p);
         ++sp;
     } else if (op < 64) {
         float b = vs[sp - 1], a = vs[sp - 2], r;
-        float k = n.f[0];
+        float k = fargs[0];
         switch (op) {
         case RRTE_SDF_UNION: r = smn(a, b); break;
         case RRTE_SDF_DIFFERENCE: r = smx(a, -b); break;
@@ -281,7 +337,7 @@ __device__ __forceinline__ void sdf_node_step(G& g, const rrte_sdf_node& n, floa
     } else if (op < 96) {
         ps[pp] = p;
         ++pp;
-        p = sdf_deform(g, op, n.i, n.f, p);
+        p = sdf_deform(g, op, iargs, fargs, p);
     } else {
         --pp;
         p = ps[pp];
@@ -296,12 +352,12 @@ __device__ __forceinline__ void sdf_node_step(G& g, const rrte_sdf_node& n, floa
 // formula reduces to a + 0 / -(-a + 0)).  Wave-uniform: taken only when every active lane may take
 // it, so the result never depends on the guard.
 template <class G>
-__device__ __forceinline__ bool sdf_guard(G& gp, const rrte_sdf_node& g, float a, f3 p, float& r) {
-    const float dx = p.x - g.f[4], dy = p.y - g.f[5], dz = p.z - g.f[6];
+__device__ __forceinline__ bool sdf_guard(G& gp, uint32_t gop, const float* gf, float a, f3 p, float& r) {
+    const float dx = p.x - gf[4], dy = p.y - gf[5], dz = p.z - gf[6];
     const float s = __builtin_amdgcn_sqrtf((dx * dx + dy * dy) + dz * dz);
-    const float L = g.f[8] * (s - g.f[7]);
-    bool ok = s >= g.f[7] && s <= g.f[9];
-    switch (g.op) {
+    const float L = gf[8] * (s - gf[7]);
+    bool ok = s >= gf[7] && s <= gf[9];
+    switch (gop) {
     case RRTE_SDF_UNION:
         ok = ok && L >= a;
         r = a;
@@ -311,12 +367,12 @@ __device__ __forceinline__ bool sdf_guard(G& gp, const rrte_sdf_node& g, float a
         r = a;
         break;
     case RRTE_SDF_SMOOTH_UNION:
-        ok = ok && sclamp(0.5f + gp.div(0.5f * (L - a), g.f[0]), 0.0f, 1.0f) == 1.0f;
+        ok = ok && sclamp(0.5f + gp.div(0.5f * (L - a), gf[0]), 0.0f, 1.0f) == 1.0f;
         r = a + 0.0f;
         break;
     default: {  // RRTE_SDF_SMOOTH_DIFFERENCE: -smin(-a, b, k)
         const float na = -a;
-        ok = ok && sclamp(0.5f + gp.div(0.5f * (L - na), g.f[0]), 0.0f, 1.0f) == 1.0f;
+        ok = ok && sclamp(0.5f + gp.div(0.5f * (L - na), gf[0]), 0.0f, 1.0f) == 1.0f;
         r = -(na + 0.0f);
         break;
     }
@@ -340,12 +396,12 @@ struct SdfProgram {
         for (uint32_t i = 0; i < count; ++i) {
             const uint32_t link = nodes[i].i[2];
             float r;
-            if (link != 0u && sdf_guard(g, nodes[link - 1u], vs[sp - 1], p, r)) {
+            if (link != 0u && sdf_guard(g, nodes[link - 1u].op, nodes[link - 1u].f, vs[sp - 1], p, r)) {
                 vs[sp - 1] = r;
                 i = link - 1u;  // continue after the op
                 continue;
             }
-            sdf_node_step(g, nodes[i], vs, ps, sp, pp, p);
+            sdf_node_step(g, nodes[i].op, nodes[i].i, nodes[i].f, vs, ps, sp, pp, p);
         }
         return vs[0];
     }
@@ -411,34 +467,62 @@ constexpr float sdf_leaf_scale(const rrte_sdf_node* n, uint32_t count) {
 // constexpr scene, unrolled at compile time; ops fold, stack slots become
 // fixed registers.  A guarded operand [I, J) becomes a uniform branch around
 // its straight-line code.
+template <class S, uint32_t K>
+constexpr TopoNode node_topo() {
+    if constexpr (S::kTopo) return S::topo_nodes[K];
+    else return TopoNode{S::nodes[K].op, {S::nodes[K].i[0], S::nodes[K].i[1], S::nodes[K].i[2]}};
+}
 template <class S, uint32_t FIRST, uint32_t I, uint32_t END, bool CHECK, class G>
-__device__ __forceinline__ void sdf_static_range(G& gp, float* vs, f3* ps, uint32_t& sp, uint32_t& pp, f3& p) {
+__device__ __forceinline__ void sdf_static_range(const S& sc, G& gp, float* vs, f3* ps, uint32_t& sp, uint32_t& pp,
+                                                 f3& p) {
     if constexpr (I < END) {
-        constexpr rrte_sdf_node n = S::nodes[FIRST + I];
-        constexpr uint32_t link = n.i[2];
+        constexpr TopoNode tn = node_topo<S, FIRST + I>();
+        constexpr uint32_t link = tn.i[2];
         if constexpr (CHECK && link != 0u) {
-            constexpr rrte_sdf_node g = S::nodes[FIRST + link - 1u];
+            constexpr uint32_t gop = node_topo<S, FIRST + link - 1u>().op;
             float r;
-            if (sdf_guard(gp, g, vs[sp - 1], p, r)) vs[sp - 1] = r;
-            else sdf_static_range<S, FIRST, I, link, false>(gp, vs, ps, sp, pp, p);
-            sdf_static_range<S, FIRST, link, END, true>(gp, vs, ps, sp, pp, p);
+            bool taken;
+            if constexpr (S::kTopo) {
+                taken = sdf_guard(gp, gop, sc.nodes[FIRST + link - 1u].f, vs[sp - 1], p, r);
+            } else {
+                constexpr rrte_sdf_node g = S::nodes[FIRST + link - 1u];
+                taken = sdf_guard(gp, gop, g.f, vs[sp - 1], p, r);
+            }
+            if (taken) vs[sp - 1] = r;
+            else sdf_static_range<S, FIRST, I, link, false>(sc, gp, vs, ps, sp, pp, p);
+            sdf_static_range<S, FIRST, link, END, true>(sc, gp, vs, ps, sp, pp, p);
         } else {
-            sdf_node_step(gp, n, vs, ps, sp, pp, p);
-            sdf_static_range<S, FIRST, I + 1u, END, true>(gp, vs, ps, sp, pp, p);
+            if constexpr (S::kTopo) {
+                sdf_node_step(gp, tn.op, tn.i, sc.nodes[FIRST + I].f, vs, ps, sp, pp, p);
+            } else {
+                constexpr rrte_sdf_node n = S::nodes[FIRST + I];
+                sdf_node_step(gp, n.op, n.i, n.f, vs, ps, sp, pp, p);
+            }
+            sdf_static_range<S, FIRST, I + 1u, END, true>(sc, gp, vs, ps, sp, pp, p);
         }
     }
 }
 
 template <class S, uint32_t FIRST, uint32_t COUNT>
 struct SdfStaticProgram {
-    static constexpr float kLeafScale = sdf_leaf_scale(S::nodes + FIRST, COUNT);
+    const S& sc;
     static constexpr bool kSmall = COUNT <= 8u;
+    // the secant exit's leaf scale (sdf_leaf_scale): folded for a full scene, the host's value in the
+    // program's first node's spare slot f[11] for a topology scene (rrte_hip.hip upload_scene)
+    __device__ __forceinline__ float leaf_scale() const {
+        if constexpr (S::kTopo) {
+            return sc.nodes[FIRST].f[11];
+        } else {
+            constexpr float k = sdf_leaf_scale(S::nodes + FIRST, COUNT);
+            return k;
+        }
+    }
     template <class G>
     __device__ __forceinline__ float eval(f3 p, G& g) const {
         float vs[RRTE_SDF_MAX_STACK];
         f3 ps[RRTE_SDF_MAX_POINT_STACK];
         uint32_t sp = 0, pp = 0;
-        sdf_static_range<S, FIRST, 0u, COUNT, true>(g, vs, ps, sp, pp, p);
+        sdf_static_range<S, FIRST, 0u, COUNT, true>(sc, g, vs, ps, sp, pp, p);
         return vs[0];
     }
     __device__ __forceinline__ float operator()(f3 p) const {
@@ -485,6 +569,11 @@ __device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float
 #ifndef RRTE_MARCH_UNROLL
 #define RRTE_MARCH_UNROLL 1
 #endif
+// RRTE_MARCH_PRED (A/B switch, bit-exact at every level; tools/r03_ab.sh): 0 divergent-exit march loops
+// (default); 1 the predicated loop (sdf_march_loop) after the divergent bound test; 2 + a predicated
+// bound test (the loop runs under the caller's EXEC); 3 + predicated shadow rays (every lane of the
+// wave runs every any-hit test).  Measured on the headline (two interleaved rounds each): 1 = lone
+// launch -6 %, frame stream +1.5 %; 3 = frame stream +9 %, lone launch unchanged.
 #ifndef RRTE_MARCH_PRED
 #define RRTE_MARCH_PRED 0
 #endif
@@ -527,7 +616,7 @@ __device__ __forceinline__ bool sdf_march_loop(const DPrim& pr, const EVAL& eval
     [[maybe_unused]] float E = 0.0f, D3 = 0.0f, dp = __builtin_nanf(""), tp = t;
     if constexpr (CONVEX) {
         E = eps * (1.0f + 0x1p-20f);
-        constexpr float K = EVAL::kLeafScale;
+        const float K = eval.leaf_scale();
         D3 = 3.0f * 0x1p-17f *
              ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
               ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
@@ -567,7 +656,7 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     f3 oc = vsub(r.o, bc);
     float b = vdot(oc, r.d);
     float cc = vdot(oc, oc) - br * br;
-#if RRTE_MARCH_PRED
+#if RRTE_MARCH_PRED >= 2
     // Predicated bound test: no divergent early return -- every lane of the caller's EXEC computes the
     // entry and exit parameters, `enter` says whether it marches (the same decisions as the branches
     // below), and the march loop runs under the caller's EXEC with the marching lanes in `live`.
@@ -597,13 +686,17 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     if (t > tend) return false;
     const float eps = pr.sdf_hit_eps, scale = pr.sdf_step_scale;
     const uint32_t steps = pr.sdf_max_steps;
+#if RRTE_MARCH_PRED == 1
+    // the predicated loop under the EXEC of the lanes that passed the bound test
+    return sdf_march_loop<EVAL, CONVEX>(pr, eval, r, t, tend, __builtin_amdgcn_ballot_w64(true), t_hit);
+#endif
     // One divergent exit per step (hit, or the next t leaves the bound) instead of three: same
     // t sequence and result as "if (d < eps*t) hit; t += d*scale; if (t > tend) miss" (NaN
     // included).  (A fully predicated form with a wave-uniform exit was measured slower.)
     bool hit = false;
     if constexpr (CONVEX) {
         const float E = eps * (1.0f + 0x1p-20f);
-        constexpr float K = EVAL::kLeafScale;
+        const float K = eval.leaf_scale();
         const float D3 = 3.0f * 0x1p-17f *
                          ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
                           ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
@@ -1098,10 +1191,17 @@ __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray&
 
 // Compile-time object index (scene-specialised kernel): only the object's
 // own intersector is instantiated.
+// Convexity of object I's SDF program for the secant early miss (sdf_convex): decided at compile time
+// from the constant program for a full scene, by the host for a topology scene (its topology key).
+template <class S, uint32_t I>
+constexpr bool prim_convex() {
+    if constexpr (S::kTopo) return S::topo_prims[I].convex;
+    else return sdf_convex(S::nodes + S::prims[I].sdf_first, S::prims[I].sdf_count);
+}
 template <bool NEED_HIT, class S, uint32_t I, bool ANY = false>
-__device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, float t_min, float t_max, Hit& out) {
-    constexpr DPrim pr = S::prims[I];
-    constexpr uint32_t kind = pr.kind;
+__device__ __forceinline__ bool intersect_at(const S& sc, UC<I> ii, const Ray& r, float t_min, float t_max, Hit& out) {
+    const DPrim pr = prim_at(sc, ii);
+    constexpr uint32_t kind = prim_kind<S, I>();
     if constexpr (kind == RRTE_PRIM_SPHERE) return isect_sphere<NEED_HIT, ANY>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_PLANE) return isect_plane<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_TRIANGLE) return isect_triangle<NEED_HIT>(pr, r, t_min, t_max, out);
@@ -1110,10 +1210,9 @@ __device__ __forceinline__ bool intersect_at(const S& sc, UC<I>, const Ray& r, f
     else if constexpr (kind == RRTE_PRIM_CONE) return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_CAPSULE) return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_SDF)
-        return isect_sdf<NEED_HIT, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>, ANY,
-                         (ANY ? kSecantExit >= 1 : kSecantExit >= 2) &&
-                             sdf_convex(S::nodes + pr.sdf_first, pr.sdf_count)>(
-            pr, SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t_min, t_max, out);
+        return isect_sdf<NEED_HIT, SdfStaticProgram<S, prim_first<S, I>(), prim_count<S, I>()>, ANY,
+                         (ANY ? kSecantExit >= 1 : kSecantExit >= 2) && prim_convex<S, I>()>(
+            pr, SdfStaticProgram<S, prim_first<S, I>(), prim_count<S, I>()>{sc}, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_MESH) return isect_mesh<ANY>(pr, sc.mesh, r, t_min, t_max, out);
     else return false;
 }
@@ -1166,13 +1265,13 @@ __device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray
 template <class S, uint32_t I>
 __device__ __forceinline__ void attributes_at(const S& sc, UC<I> ii, const Ray& r, float t_min, float t, uint32_t sub,
                                               Hit& out) {
-    constexpr DPrim pr = S::prims[I];
-    if constexpr (pr.kind == RRTE_PRIM_SDF)
-        sdf_hit_attributes(SdfStaticProgram<S, pr.sdf_first, pr.sdf_count>{}, r, t, out);
-    else if constexpr (pr.kind == RRTE_PRIM_MESH)
+    constexpr uint32_t kind = prim_kind<S, I>();
+    if constexpr (kind == RRTE_PRIM_SDF)
+        sdf_hit_attributes(SdfStaticProgram<S, prim_first<S, I>(), prim_count<S, I>()>{sc}, r, t, out);
+    else if constexpr (kind == RRTE_PRIM_MESH)
         mesh_tri_hit(sc.mesh, sub, r, t_min, kInf, out);
-    else if constexpr (pr.kind == RRTE_PRIM_SPHERE)
-        sphere_attributes(pr, r, t, out);
+    else if constexpr (kind == RRTE_PRIM_SPHERE)
+        sphere_attributes(prim_at(sc, ii), r, t, out);
     else
         intersect_at<true>(sc, ii, r, t_min, kInf, out);
 }
@@ -1229,7 +1328,7 @@ __device__ __forceinline__ bool occluded(const S& sc, const Ray& r, float t_min,
         // one wave-uniform skip test: culled, or every lane already occluded (mask cleared)
         if (mask == 0 || (i < 64u && !((mask >> i) & 1ull))) return;
         Hit h;
-#if RRTE_MARCH_PRED
+#if RRTE_MARCH_PRED >= 3
         // predicated: every lane of the caller's EXEC runs the test (marches stay wide, see
         // sdf_march_loop); lanes that are already occluded or that cast no ray (t_max = -inf) get an
         // empty interval, for which every intersector reports no hit
@@ -1363,21 +1462,29 @@ __device__ __forceinline__ uint64_t shadow_cull(const Cull& cl, const HitBound& 
 // shadow_cull, whose per-light wave-uniform prologue (capsule axis, |AB|^2, its reciprocal, the
 // margin) every light repeated on all 64 lanes -- and one ballot carries every light's n bits.
 // Lights shadow_cull never culls (ambient; directional with a non-unit direction) get all-ones.
+// Whether shadow_cull may cull for light I (not ambient; a directional light only with a unit
+// direction): from the constant record of a full scene, by the host for a topology scene.
+constexpr bool light_record_cullable(const DLight& L) {
+#pragma clang fp contract(off)
+    if (L.kind == RRTE_LIGHT_AMBIENT) return false;
+    if (L.kind != RRTE_LIGHT_DIRECTIONAL) return true;
+    const float d2 = (L.direction[0] * L.direction[0] + L.direction[1] * L.direction[1]) + L.direction[2] * L.direction[2];
+    return (d2 - 1.0f <= 1e-3f) && (1.0f - d2 <= 1e-3f);
+}
+template <class S, uint32_t I>
+constexpr bool light_cullable() {
+    if constexpr (S::kTopo) {
+        return S::topo_lights[I].cullable;
+    } else {
+        constexpr bool c = light_record_cullable(S::lights[I]);
+        return c;
+    }
+}
 template <class S>
-__device__ __forceinline__ void shadow_cull_lanes(const Cull& cl, const HitBound& hb, uint64_t* smask) {
+__device__ __forceinline__ void shadow_cull_lanes(const S& sc, const Cull& cl, const HitBound& hb, uint64_t* smask) {
     constexpr uint32_t n = S::num_prims, nl = S::num_lights;
     static_assert(n * nl <= 64u && n > 0u, "one lane per (light, object)");
-    auto cullable = [](auto lii) {
-        constexpr DLight L = S::lights[(uint32_t)lii];
-        if constexpr (L.kind == RRTE_LIGHT_AMBIENT) return false;
-        else if constexpr (L.kind == RRTE_LIGHT_DIRECTIONAL) {
-            constexpr float d2 = (L.direction[0] * L.direction[0] + L.direction[1] * L.direction[1]) +
-                                 L.direction[2] * L.direction[2];
-            return (d2 - 1.0f <= 1e-3f) && (1.0f - d2 <= 1e-3f);
-        } else {
-            return true;
-        }
-    };
+    auto cullable = [](auto lii) { return light_cullable<S, (uint32_t)decltype(lii)::value>(); };
     if (!cull_on(cl) || hb.unsafe || !hb.any) {
         auto fill = [&](auto lii) { smask[(uint32_t)lii] = (cullable(lii) && cull_on(cl) && !hb.unsafe) ? 0ull : ~0ull; };
         static_for<0, nl>(fill);
@@ -1389,9 +1496,9 @@ __device__ __forceinline__ void shadow_cull_lanes(const Cull& cl, const HitBound
     f3 B = A;
     bool directional = false;
     auto pick = [&](auto lii) {
-        constexpr DLight L = S::lights[(uint32_t)lii];
+        const DLight L = light_at(sc, lii);
         if (l == (uint32_t)lii) {
-            if constexpr (L.kind == RRTE_LIGHT_DIRECTIONAL) {
+            if constexpr (light_kind<S, (uint32_t)decltype(lii)::value>() == RRTE_LIGHT_DIRECTIONAL) {
                 B = vsub(A, V(L.direction[0], L.direction[1], L.direction[2]));
                 directional = true;
             } else {
@@ -1658,7 +1765,7 @@ __device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray
 // LAMBERT_SHADOW (build-defined) for one camera ray.  Called by
 // all 64 lanes of the wave (`live` marks the lanes that own a pixel): with
 // CULL the hit-point bound and the per-light shadow culls are wave reductions.
-constexpr bool kShadeAll = RRTE_MARCH_PRED != 0;  // shade every lane (predicated), or only hit lanes
+constexpr bool kShadeAll = RRTE_MARCH_PRED >= 3;  // shade every lane (predicated), or only hit lanes
 template <class S, bool CULL>
 __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, const Cull& cl, const Ray& r, bool live,
                                              uint32_t& nshadow, uint32_t pmask = ~0u) {
@@ -1702,7 +1809,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             return;
         }
         const float ndl = vdot(h.n, k.dir);
-#if RRTE_MARCH_PRED
+#if RRTE_MARCH_PRED >= 3
         // predicated over every lane (hit or not): a lane that casts no shadow ray tests the empty
         // interval (t_max = -inf) along a benign direction, so the any-hit marches run wide
         const bool cast = hit && ndl > 0.0f && k.att > 0.0f;
@@ -1744,7 +1851,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             // all light masks first, at one converged point, then the shading
             uint64_t smask[S::num_lights ? S::num_lights : 1];
             if constexpr (S::num_lights > 0 && S::num_prims * S::num_lights <= 64u) {
-                shadow_cull_lanes<S>(cl, hb, smask);
+                shadow_cull_lanes<S>(sc, cl, hb, smask);
             } else {
                 const float4 bnd = cull_on(cl) ? load_bound(cl) : float4{};
                 auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii), bnd); };

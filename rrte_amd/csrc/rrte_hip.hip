@@ -170,8 +170,14 @@ struct rrte_ctx {
     bool env_wg256 = false;           // RRTE_WG64=0: specialised kernels in 256-thread workgroups (A/B only)
     int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
-    struct { uint64_t gen; int mode, jit_mode; bool cull, single, valid; JitKernel* k; } jit_last{};
+    struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, valid; JitKernel* k; } jit_last{};
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
+    // topology kernels (jit.hip JitTopo): the cached scene's topology key and structural decisions, and
+    // how many consecutive scene changes kept that topology (value edits: an animation)
+    int env_jit_topo = 2;                        // RRTE_JIT_TOPO: 0 full only, 1 topology only, 2 adaptive
+    std::string topo_key;
+    JitTopo topo;
+    uint64_t value_edits = 0;
     std::vector<DPrim> h_prims;                  // host copy of the lowered scene (JIT source)
     std::vector<float4> h_bounds;                // host copy of the per-object culling spheres
     std::vector<DMaterial> h_mats;
@@ -522,6 +528,46 @@ bool scene_same(const rrte_ctx* c, const rrte_scene_ir* s) {
     return true;
 }
 
+// The scene's topology -- what a topology kernel compiles in (jit.hip, ray_kernels.hpp TopoPrim /
+// TopoNode / TopoLight) -- as a key, with its structural decisions in `topo`: object kinds and SDF
+// node ranges, node ops and integer arguments (CSG-guard links included), light kinds, per-object
+// SDF convexity (value-dependent for cones) and per-light cullability.  Also stores each SDF
+// program's leaf scale (sdf_leaf_scale, the secant exit's error bound) in its first node's spare
+// slot f[11], where a topology kernel reads it; no other code reads f[11].
+std::string topology_of(const std::vector<DPrim>& prims, const std::vector<DLight>& lights,
+                        std::vector<rrte_sdf_node>& nodes, JitTopo& topo) {
+    std::string key;
+    auto put = [&](uint32_t v) { key.append(reinterpret_cast<const char*>(&v), sizeof v); };
+    put((uint32_t)prims.size());
+    put((uint32_t)lights.size());
+    put((uint32_t)nodes.size());
+    topo.convex.assign(prims.size(), 0);
+    topo.cullable.assign(lights.size(), 0);
+    for (size_t i = 0; i < prims.size(); ++i) {
+        const DPrim& p = prims[i];
+        put(p.kind);
+        put(p.sdf_first);
+        put(p.sdf_count);
+        if (p.kind == RRTE_PRIM_SDF && p.sdf_count && (size_t)p.sdf_first + p.sdf_count <= nodes.size()) {
+            topo.convex[i] = sdf_convex(&nodes[p.sdf_first], p.sdf_count) ? 1 : 0;
+            nodes[p.sdf_first].f[11] = sdf_leaf_scale(&nodes[p.sdf_first], p.sdf_count);
+        }
+        put(topo.convex[i]);
+    }
+    for (const rrte_sdf_node& n : nodes) {
+        put(n.op);
+        put(n.i[0]);
+        put(n.i[1]);
+        put(n.i[2]);
+    }
+    for (size_t i = 0; i < lights.size(); ++i) {
+        topo.cullable[i] = light_record_cullable(lights[i]) ? 1 : 0;
+        put(lights[i].kind);
+        put(topo.cullable[i]);
+    }
+    return key;
+}
+
 rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
     const size_t bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
     SceneKeyParts kparts;
@@ -576,6 +622,8 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     if ((r = put(c->d_lights, lights.data(), lights.size() * sizeof(DLight))) != RRTE_OK) return r;
     // SDF programs with their exact CSG early-outs (sdf_guard.hpp); the key above stays the caller's IR
     std::vector<rrte_sdf_node> nodes = decorate_scene_sdf(s, c->env_guard_leaves);
+    JitTopo topo;
+    std::string tkey = topology_of(prims, lights, nodes, topo);
     if ((r = put(c->d_nodes, nodes.data(), bn)) != RRTE_OK) return r;
     if ((r = put(c->d_bounds, bounds.data(), bounds.size() * sizeof(float4))) != RRTE_OK) return r;
     if ((r = put(c->d_mesh_nodes, md.nodes.data(), md.nodes.size() * sizeof(float4))) != RRTE_OK) return r;
@@ -595,6 +643,9 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     c->h_mats = mats;
     c->h_lights = lights;
     c->h_nodes = std::move(nodes);
+    c->value_edits = (!c->topo_key.empty() && tkey == c->topo_key) ? c->value_edits + 1 : 0;
+    c->topo_key = std::move(tkey);
+    c->topo = std::move(topo);
     c->n_prims = s->num_prims;
     c->n_mats = s->num_materials;
     c->n_lights = s->num_lights;
@@ -772,34 +823,35 @@ bool cull_policy(const rrte_scene_ir* s, uint32_t mode, int env_cull) {
 // JIT policy says so; nullptr = use the generic kernel.
 constexpr uint32_t kJitMaxPrims = 128, kJitMaxNodes = 1024;
 
-JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
-    if (c->jit_mode == RRTE_JIT_OFF) return nullptr;
-    auto& last = c->jit_last;  // per-frame fast path: same scene, mode and policy as the last frame
-    if (last.valid && last.gen == c->scene_gen && last.mode == mode && last.cull == cull && last.single == single &&
-        last.jit_mode == c->jit_mode)
-        return last.k;
-    if (c->h_prims.size() > kJitMaxPrims || c->h_nodes.size() > kJitMaxNodes) return nullptr;
-    std::string key(c->scene_key.begin(), c->scene_key.end());
+// FULL or TOPOLOGY kernel (RRTE_JIT_TOPO, rrte_hip.h).  Adaptive: topology while the scene's values keep
+// changing under one topology (one compile for a whole animation), full once the scene has been
+// rendered unchanged for kJitFullAfter frames (until that full kernel is ready, the topology kernel).
+constexpr uint64_t kJitFullAfter = 16;
+
+bool jit_wants_topology(const rrte_ctx* c) {
+    return c->env_jit_topo == 1 ||
+           (c->env_jit_topo == 2 && c->value_edits >= 1 && c->same_scene_renders < kJitFullAfter);
+}
+
+std::string jit_key(const rrte_ctx* c, bool topo, int mode, bool cull, bool single) {
+    std::string key(1, topo ? 'T' : 'F');
+    if (topo) key += c->topo_key;
+    else key.append(c->scene_key.begin(), c->scene_key.end());
     key.push_back((char)mode);
     key.push_back((char)cull);
     key.push_back((char)single);
-    auto remember = [&](JitKernel* k) {
-        last.gen = c->scene_gen;
-        last.mode = mode;
-        last.jit_mode = c->jit_mode;
-        last.cull = cull;
-        last.single = single;
-        last.k = k;
-        last.valid = true;
-        return k;
-    };
+    return key;
+}
+
+// The cached kernel for `key`, compiling it if the JIT policy says so; nullptr = not available (yet).
+JitKernel* jit_lookup(rrte_ctx* c, const std::string& key, bool topo, int mode, bool cull, bool single) {
     auto it = c->jit_cache.find(key);
-    if (it != c->jit_cache.end()) return remember(it->second.fn ? &it->second : nullptr);
+    if (it != c->jit_cache.end()) return it->second.fn ? &it->second : nullptr;
     JitKernel jk;
     std::string log;
     auto pend = c->jit_pending.find(key);
     if (pend != c->jit_pending.end()) {
-        // AUTO: a background compile of this scene is running; keep the generic kernel until it lands
+        // AUTO: a background compile of this kernel is running; keep the current kernel until it lands
         if (pend->second.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return nullptr;
         const JitCode jc = pend->second.get();
         c->jit_pending.erase(pend);
@@ -810,21 +862,22 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
             c->stats.jit_compile_ms = jk.compile_ms;
         }
     } else {
-        if (!(c->jit_mode == RRTE_JIT_ON || c->same_scene_renders >= 1)) return nullptr;
+        if (!(c->jit_mode == RRTE_JIT_ON || c->same_scene_renders >= 1 || topo)) return nullptr;
         if (c->jit_cache.size() >= 32) {
             // frames launched from these modules may still run on caller streams (a mode / cull /
             // sample-count change does not re-upload the scene, so upload_scene's sync has not run)
             if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
             for (auto& kv : c->jit_cache) jit_release(kv.second);
             c->jit_cache.clear();
-            last.valid = false;
+            c->jit_last.valid = false;
         }
         std::string src = jit_source(c->h_prims.data(), (uint32_t)c->h_prims.size(), c->h_mats.data(),
                                      (uint32_t)c->h_mats.size(), c->h_lights.data(), (uint32_t)c->h_lights.size(),
-                                     c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull, single);
+                                     c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull, single,
+                                     topo ? &c->topo : nullptr);
         if (c->env_wg256) src = "#define RRTE_WG256 1\n" + src;
         if (c->jit_mode == RRTE_JIT_AUTO) {
-            // compile on a background thread (hiprtc only); frames keep running on the generic kernel
+            // compile on a background thread (hiprtc only); frames keep running on the current kernel
             c->jit_pending.emplace(key, std::async(std::launch::async, [src]() { return jit_compile_code(src); }));
             return nullptr;
         }
@@ -835,9 +888,40 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
             c->stats.jit_compile_ms = jk.compile_ms;
         }
     }
+    jk.topology = topo;
     auto& slot = c->jit_cache[key];
     slot = jk;
-    return remember(slot.fn ? &slot : nullptr);
+    return slot.fn ? &slot : nullptr;
+}
+
+JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
+    if (c->jit_mode == RRTE_JIT_OFF) return nullptr;
+    auto& last = c->jit_last;  // per-frame fast path: same scene, mode, policy and kernel kind as the last frame
+    const bool topo = jit_wants_topology(c);
+    if (last.valid && last.gen == c->scene_gen && last.mode == mode && last.cull == cull && last.single == single &&
+        last.jit_mode == c->jit_mode && last.topo == topo)
+        return last.k;
+    if (c->h_prims.size() > kJitMaxPrims || c->h_nodes.size() > kJitMaxNodes) return nullptr;
+    const std::string key = jit_key(c, topo, mode, cull, single);
+    JitKernel* k = jit_lookup(c, key, topo, mode, cull, single);
+    if (!k && !c->jit_cache.count(key)) {
+        // not available yet (AUTO: not due, or compiling in the background): not remembered, asked again
+        // next frame.  The full kernel of a scene that stopped changing: its topology kernel meanwhile
+        if (!topo && c->env_jit_topo == 2 && c->value_edits >= 1) {
+            auto it = c->jit_cache.find(jit_key(c, true, mode, cull, single));
+            if (it != c->jit_cache.end() && it->second.fn) return &it->second;
+        }
+        return nullptr;
+    }
+    last.gen = c->scene_gen;
+    last.mode = mode;
+    last.jit_mode = c->jit_mode;
+    last.cull = cull;
+    last.single = single;
+    last.topo = topo;
+    last.k = k;
+    last.valid = true;
+    return k;
 }
 
 LaunchPlan plan_launch(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
@@ -865,11 +949,12 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     Cull cl{L.cull ? c->d_bounds : nullptr, L.num_prims};
     const dim3 grid(L.gx, L.gy, L.k.nframes), block(kBlockThreads);
     JitKernel* jk = jit_kernel_for(c, L.mode, L.cull, L.single);
-    c->stats.jit_active = jk ? 1u : 0u;
+    c->stats.jit_active = jk ? (jk->topology ? 2u : 1u) : 0u;
     if (jk) {
         unsigned long long* ctr = c->d_counters;
         MeshView mv = c->mesh_view;
-        void* args[] = {&L.k, &cl, &mv, &d_rgba, &d_f32, &ctr};
+        SceneValues vals{c->d_prims, c->d_mats, c->d_lights, c->d_nodes};  // read by topology kernels
+        void* args[] = {&L.k, &cl, &mv, &d_rgba, &d_f32, &ctr, &vals};
         HostSection hs(c);
         if (c->env_wg256)
             HIPCHK(c, hipModuleLaunchKernel(jk->fn, (L.k.width + 15) / 16, (L.k.rows + 15) / 16, grid.z, 256, 1, 1, 0,
@@ -1093,6 +1178,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_COMM_TIMEOUT_MS")) c->comm_timeout_ms = std::max<uint32_t>(1u, (uint32_t)strtoul(g, nullptr, 0));
     if (const char* g = getenv("RRTE_FAULT_STALL_GATHER")) c->fault_stall_at = strtoull(g, nullptr, 0);
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
+    if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
         if (sscanf(e, "%d:%d", &n, &r) == 2 && n > 1 && r >= 0 && r < n) {
@@ -1296,10 +1382,16 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
     // spp > 1 or max_depth > 1) instead of the straight-line one
     const char* mv = getenv("RRTE_JIT_CHECK_MULTI");
     const bool single = !(mv && mv[0] == '1');
-    const std::vector<rrte_sdf_node> nodes = decorate_scene_sdf(s, env_guard_setting());
+    std::vector<rrte_sdf_node> nodes = decorate_scene_sdf(s, env_guard_setting());
+    JitTopo topo;
+    topology_of(prims, lights, nodes, topo);
+    // RRTE_JIT_TOPO=1: the topology kernel instead of the full one
+    const char* tv = getenv("RRTE_JIT_TOPO");
+    const bool want_topo = tv && tv[0] == '1';
     std::string src = jit_source(prims.data(), (uint32_t)prims.size(), mats.data(), (uint32_t)mats.size(),
                                  lights.data(), (uint32_t)lights.size(), nodes.data(), s->num_sdf_nodes, mode,
-                                 cull_policy(s, (uint32_t)mode, env_cull_setting()), single);
+                                 cull_policy(s, (uint32_t)mode, env_cull_setting()), single,
+                                 want_topo ? &topo : nullptr);
     std::string msg;
     bool ok = jit_compile_only(src, msg);
     if (log && log_len) {
@@ -1376,6 +1468,14 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
     NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
     c->nranks = nranks;
     c->rank = rank;
+    if (nranks == 1 && c->emu_nranks > 1) {
+        // RRTE_EMULATE_RANK=N:R with a 1-rank communicator (diagnostic, one GPU): the gather path lays
+        // frames out as rank R of N -- R's bands rendered into its slab slice, the 1-rank gather moving
+        // that slice, and on rank 0 the de-interleave of all N slices (the other N-1 hold whatever the
+        // receive buffer held) -- i.e. one rank's whole per-frame cost except the xGMI transfers.
+        c->nranks = c->emu_nranks;
+        c->rank = c->emu_rank;
+    }
     return RRTE_OK;
 }
 

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 RMS_TOL = 1e-4
 
 
-def compare(objs, lights, cam, cfg, linear_exact=True, threads=16, jit=abi.JIT_OFF):
+def compare(objs, lights, cam, cfg, linear_exact=True, threads=16, jit=abi.JIT_OFF, expect_jit=None):
     rt = Raytracer(cfg, device=0, jit=jit)
     g8, gf = rt.render_f32(objs, lights, [], cam)
     st = rt.stats()
@@ -40,7 +40,9 @@ def compare(objs, lights, cam, cfg, linear_exact=True, threads=16, jit=abi.JIT_O
     assert u8 <= 1, info
     assert int(st.shadow_rays) == rsh, info
     assert st.primary_rays == cfg.width * cfg.height * cfg.samples_per_pixel
-    assert st.jit_active == (1 if jit == abi.JIT_ON else 0), "unexpected kernel path"
+    if expect_jit is None:
+        expect_jit = 1 if jit == abi.JIT_ON else 0
+    assert st.jit_active == expect_jit, "unexpected kernel path"
     if linear_exact:
         assert np.array_equal(glin.view(np.uint32), rlin.view(np.uint32)), info
     return info
