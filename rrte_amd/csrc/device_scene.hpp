@@ -93,6 +93,11 @@ struct KParams {
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
     uint32_t nframes;        // frames of this launch (gridDim.z), cam[0 .. nframes)
     uint64_t frame_stride;   // bytes between consecutive frames' RGBA8 / slab outputs
+    // blocking renders with the pipelined host copy (rrte_hip.hip band_copy_kernel): each workgroup
+    // counts itself done in band_done[blockIdx.y / band_blocks] after its stores; nullptr otherwise
+    uint32_t* band_done;
+    uint32_t band_blocks;
+    uint32_t band_release;   // how a workgroup releases its stores to the band copy (ray_kernels.hpp)
     FrameCam cam[kMaxLaunchFrames];
 };
 

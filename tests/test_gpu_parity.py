@@ -335,14 +335,16 @@ def test_camera_tile_culling_with_band_mapping(band, jit, monkeypatch):
         ctx.close()
 
 
-def test_jit_cache_eviction_with_frames_in_flight():
+def test_jit_cache_eviction_with_frames_in_flight(monkeypatch):
     """The scene-specialised kernel cache holds 32 modules; the 33rd (scene, mode, variant) evicts
     them all.  A mode or sample-count change does not re-upload the scene (upload_scene's device sync
     does not run), so the eviction itself must wait for frames still running from the old modules on
     other streams.  Nine small scenes x up to four variants, every frame on one of four
     streams without synchronising in between, the 33rd module requested on a same-scene variant
-    switch; every frame must equal the generic kernel's."""
+    switch; every frame must equal the generic kernel's.  Full kernels only (RRTE_JIT_TOPO=0): the
+    nine scenes differ in values only, so the adaptive policy would share one topology kernel."""
     import torch
+    monkeypatch.setenv("RRTE_JIT_TOPO", "0")
     W, H = 48, 32
     variants = [("refcompat", 1), ("refcompat", 2), ("lambert_shadow", 1), ("lambert_shadow", 2)]
     plan = []
