@@ -23,7 +23,7 @@ import numpy as np
 # Frames in flight need their streams on distinct hardware queues.  HIP's default is 4 per process (the
 # GPU box exports GPU_MAX_HW_QUEUES=4), shared with torch's and the library's own streams; one rank of
 # an 8-GPU job then needs ~40 us for its share of a frame instead of ~24 us with 32 queues
-# (tools/r02_inflight.sh, 20 steps; the one-GPU frame is the same with 4 or 32).  The bench's own
+# (tools/runs/r02_inflight.sh, 20 steps; the one-GPU frame is the same with 4 or 32).  The bench's own
 # setting is RRTE_BENCH_HW_QUEUES (default 32), applied before HIP starts; the value in effect is
 # recorded in the JSON line (config.hw_queues).  Under rocprofv3 the profiler starts HIP before this
 # line runs, so the profiling scripts export GPU_MAX_HW_QUEUES themselves.
@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
                          "so one frame's tail overlaps the next frame's start (1 = strictly one after another); "
-                         "default 4 on one GPU (tools/r02_inflight.sh); N > 1: frames per gather batch, default 8")
+                         "default 4 on one GPU (tools/runs/r02_inflight.sh); N > 1: frames per gather batch, default 8")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
@@ -320,7 +320,7 @@ def main():
     if spin:
         # poll for the end of the work (events on every stream the frames and the library used)
         # before the closing synchronize: a blocking device synchronize wakes the host ~40 us after
-        # the last kernel ends (tools/r02_timeline2.sh); the work measured is the same
+        # the last kernel ends (tools/runs/r02_timeline2.sh); the work measured is the same
         ends = [torch.cuda.Event() for _ in streams]
         for e, s in zip(ends, streams):
             e.record(s)

@@ -93,11 +93,6 @@ struct KParams {
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
     uint32_t nframes;        // frames of this launch (gridDim.z), cam[0 .. nframes)
     uint64_t frame_stride;   // bytes between consecutive frames' RGBA8 / slab outputs
-    // blocking renders with the pipelined host copy (rrte_hip.hip band_copy_kernel): each workgroup
-    // counts itself done in band_done[blockIdx.y / band_blocks] after its stores; nullptr otherwise
-    uint32_t* band_done;
-    uint32_t band_blocks;
-    uint32_t band_release;   // how a workgroup releases its stores to the band copy (ray_kernels.hpp)
     FrameCam cam[kMaxLaunchFrames];
 };
 
@@ -111,6 +106,32 @@ constexpr uint32_t kFlagSlabRgb24 = 1u << 31;
 struct f3 { float x, y, z; };
 
 __device__ __forceinline__ f3 V(float x, float y, float z) { return f3{x, y, z}; }
+// Out-of-range fallback of the short correctly rounded sequences below: a divergent branch around the
+// compiler's full sequence (an EXEC save, branch and restore on the scalar unit per call), or with
+// RRTE_GUARD_UNIFORM a wave-uniform branch on the ballot of the out-of-range lanes that runs the full
+// sequence on every lane and selects it for the flagged ones (bit-identical either way).
+#ifndef RRTE_GUARD_UNIFORM
+#define RRTE_GUARD_UNIFORM 0
+#endif
+#define RRTE_FALLBACK(bad, r, full)                                                            \
+    do {                                                                                       \
+        if (RRTE_GUARD_UNIFORM) {                                                              \
+            const uint64_t m_ = __builtin_amdgcn_ballot_w64(bad);                              \
+            if (__builtin_expect(m_ != 0ull, 0)) r = mask_select(m_, r, (full));               \
+        } else if (__builtin_expect((bad), 0)) {                                               \
+            r = (full);                                                                        \
+        }                                                                                      \
+    } while (0)
+// Lane select on a wave mask held in SGPRs: lane i gets `b` if bit i of m is set, else `a` -- one
+// v_cndmask_b32 reading the mask directly (what __builtin_amdgcn_inverse_ballot_w64 lowers to; the
+// hiprtc front end of this ROCm does not know that builtin).
+__device__ __forceinline__ float mask_select(uint64_t m, float a, float b) {
+    float r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+__device__ __forceinline__ bool mask_lane(uint64_t m) { return mask_select(m, 0.0f, 1.0f) != 0.0f; }
+
 // Correctly rounded f32 sqrt (Rust f32::sqrt), 7 VALU ops with its guard instead of the compiler's 16.
 // Verified bit-identical to __builtin_sqrtf over all 2^32 inputs on gfx950 (rrte_hip_fpcheck,
 // tests/test_gpu_fpexact.py).  (Round 1's form -- the neighbour of v_sqrt_f32 whose residual
@@ -137,7 +158,7 @@ __device__ __forceinline__ float sqrt_rn(float x) {
     // inputs below 2^-96 come out wrong, tests/test_gpu_fpexact.py)
     constexpr uint32_t kLo = 0x0F800000u, kInf = 0x7F800000u;  // bits of 2^-96 and +inf
 #ifndef RRTE_ABLATE_NO_GUARDS  // timing experiment only: drops the out-of-range fallback branches
-    if (__builtin_expect(__float_as_uint(x) - kLo >= kInf - kLo, 0)) r = __builtin_sqrtf(x);
+    RRTE_FALLBACK(__float_as_uint(x) - kLo >= kInf - kLo, r, __builtin_sqrtf(x));
 #endif
     return r;
 }
@@ -150,7 +171,7 @@ __device__ __forceinline__ float rcp_rn(float b) {
     float y = __builtin_amdgcn_rcpf(b);
     y = __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
 #ifndef RRTE_ABLATE_NO_GUARDS
-    if (__builtin_expect(!(__builtin_fabsf(b) >= 0x1.0p-126f && __builtin_fabsf(b) <= 0x1.0p+126f), 0)) y = 1.0f / b;
+    RRTE_FALLBACK(!(__builtin_fabsf(b) >= 0x1.0p-126f && __builtin_fabsf(b) <= 0x1.0p+126f), y, 1.0f / b);
 #endif
     return y;
 }
@@ -169,22 +190,12 @@ __device__ __forceinline__ float div_rn(float a, float b) {
     if (__builtin_constant_p(b) && __builtin_fabsf(b) >= 0x1.0p-60f && __builtin_fabsf(b) <= 0x1.0p+60f) {
         float r = div_by_rcp(a, b, 1.0f / b);
 #ifndef RRTE_ABLATE_NO_GUARDS
-        if (__builtin_expect(!(__builtin_fabsf(a) >= 0x1.0p-60f && __builtin_fabsf(a) <= 0x1.0p+60f), 0)) r = a / b;
+        RRTE_FALLBACK(!(__builtin_fabsf(a) >= 0x1.0p-60f && __builtin_fabsf(a) <= 0x1.0p+60f), r, a / b);
 #endif
         return r;
     }
     return a / b;
 }
-// Lane select on a wave mask held in SGPRs: lane i gets `b` if bit i of m is set, else `a` -- one
-// v_cndmask_b32 reading the mask directly (what __builtin_amdgcn_inverse_ballot_w64 lowers to; the
-// hiprtc front end of this ROCm does not know that builtin).
-__device__ __forceinline__ float mask_select(uint64_t m, float a, float b) {
-    float r;
-    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
-    return r;
-}
-__device__ __forceinline__ bool mask_lane(uint64_t m) { return mask_select(m, 0.0f, 1.0f) != 0.0f; }
-
 // Guard policies of the SDF evaluation (ray_kernels.hpp: sdf_leaf ... SdfStaticProgram::eval).
 // GuardNow: sqrt_rn / div_rn as above, each with its own divergent fallback branch (an EXEC save,
 // branch and restore on the scalar unit per call).  GuardDefer: the same short sequences, but each

@@ -15,8 +15,6 @@ namespace rrte {
 constexpr float kInf = __builtin_huge_valf();
 constexpr uint32_t kCounterShards = 256;  // shadow-ray counter shards (power of two)
 constexpr uint32_t kCounterStride = 16;   // u64 per shard: one 128-B line each
-constexpr uint32_t kBandShards = 8;       // band-done counters per row band (blocking renders' pipelined copy)
-constexpr uint32_t kBandStride = 32;      // u32 per band-done counter: one 128-B line each
 
 // Runtime scene: device pointers + counts (the generic kernel).  A
 // scene-specialised kernel (jit.cpp, hiprtc) instead passes a struct whose
@@ -2054,9 +2052,6 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
                 b[0] = (uint8_t)px;
                 b[1] = (uint8_t)(px >> 8);
                 b[2] = (uint8_t)(px >> 16);
-            } else if (kp.band_done && kp.band_release == 2u) {
-                // write-through store (the band copy reads it from another XCD; no L2 write-back needed)
-                __hip_atomic_store(out_rgba8 + o, px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             } else {
                 out_rgba8[o] = px;
             }
@@ -2083,22 +2078,6 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
             const uint32_t shard = (blockIdx.x + blockIdx.y * gridDim.x + threadIdx.x / 64u * 61u) & (kCounterShards - 1u);
             atomicAdd(counters + shard * kCounterStride, (unsigned long long)v);
         }
-    }
-    if (kp.band_done) {
-        // release this workgroup's pixel stores to the concurrent band copy, then count the workgroup
-        // done in its band (only blocking renders with the pipelined host copy pass band_done).
-        // band_release: 0 seq_cst agent fence (L2 write-back + invalidate), 1 release fence (write-back),
-        // 2 the stores above were write-through: wait for their acknowledgements only
-        if (kp.band_release == 0u) __threadfence();
-        else if (kp.band_release == 1u) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        else __builtin_amdgcn_s_waitcnt(0);
-        if constexpr (!kWg64) __syncthreads();
-        // each band's count is spread over kBandShards counters on their own 128-B lines (a band's ~1000
-        // workgroups on one line serialise at the memory side, as one shadow-ray counter did)
-        if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(kp.band_done + ((blockIdx.y / kp.band_blocks) * kBandShards +
-                                                   (blockIdx.x & (kBandShards - 1u))) * kBandStride,
-                                   1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (stamps && lane == 0) {
         const uint64_t t1 = wall_clock64();

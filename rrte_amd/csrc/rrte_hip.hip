@@ -97,6 +97,7 @@ struct rrte_ctx {
     struct Batch {
         uint32_t n = 0, cap = 0;             // frames planned into it / frames it was opened for
         uint32_t rendered = 0;               // frames [0, rendered) already launched into the send slab
+        bool inplace = false;                // root, rendered at the flush: into its slot of the receive slab
         uint32_t width = 0, height = 0, band = 0;
         int root = 0;
         bool rgb24 = false;
@@ -130,43 +131,10 @@ struct rrte_ctx {
     uint64_t fault_stall_at = 0;
     uint32_t* h_stall = nullptr;       // pinned, device-visible release flag
     bool stall_armed = false;
-    // Blocking drop-in path (rrte_hip_render into a host buffer, Raytracer::render's signature).  The
-    // frame renders into HBM; every workgroup counts itself done in its row band (KParams::band_done);
-    // a copy kernel on a second stream, running alongside the render, moves each band into pinned host
-    // memory mapped to the device as soon as the band is complete (wide stores over PCIe, ~52 GB/s,
-    // tools/micro/d2h.hip) and raises a per-part flag in host memory; host threads copy each band into
-    // the caller's buffer as its flags appear.  The frame's PCIe transfer thus overlaps the render's
-    // tail instead of following it.  RRTE_BOUNDARY_PIPE=0: render, then one pageable hipMemcpy (A/B).
-    static constexpr int kCopyHelpers = 2;
-    static constexpr uint32_t kCopyParts = 8;  // copy workgroups (and host flags) per band
-    bool boundary_pipe = true;
-    uint32_t env_band_release = 2;     // RRTE_BAND_RELEASE (A/B): KParams::band_release
-    uint8_t* h_stage = nullptr;        // pinned, mapped
-    uint8_t* d_stage = nullptr;        // its device address
-    size_t cap_stage = 0;
-    uint32_t* h_flags = nullptr;       // pinned, mapped, coherent: one per (band, part)
-    uint32_t* d_flags = nullptr;
-    uint32_t* d_band_done = nullptr;   // device: workgroups done per band
-    uint32_t cap_bands = 0;
-    hipStream_t copy_stream = nullptr;
-    hipEvent_t ev_pre = nullptr, ev_copied = nullptr;
-    uint32_t pipe_gen = 0;
-    struct { uint32_t* done; uint32_t blocks; } pipe_sig{};  // consumed by make_params during the launch
-    struct CopyJob {
-        std::mutex mu;
-        std::condition_variable cv;
-        uint64_t gen = 0;              // bumped per frame (helpers wake up)
-        bool quit = false;
-        std::atomic<int> pending{0};   // helpers still copying this frame
-        std::atomic<bool> failed{false};
-        uint8_t* dst = nullptr;
-        const uint8_t* src = nullptr;
-        size_t bytes = 0, band_bytes = 0;
-        uint32_t nbands = 0, flag_gen = 0;
-        const uint32_t* flags = nullptr;
-        hipEvent_t copied = nullptr;   // the copy kernel's completion (failure detection only)
-    } job;
-    std::vector<std::thread> helpers;
+    // Blocking drop-in path (rrte_hip_render into a host buffer, Raytracer::render's signature): render,
+    // then one pageable hipMemcpy (the runtime's path runs at PCIe rate, ~53 GB/s, tools/micro/d2h.hip).
+    // Measured and rejected: a band copy kernel beside the render, and touching the
+    // caller's fresh pages from host threads while the render runs.
     rrte_stats stats{};
     bool pending_kernel_timing = false;
     uint64_t pending_primary = 0;
@@ -178,6 +146,7 @@ struct rrte_ctx {
     bool env_tile_cull = true;    // RRTE_TILE_CULL=0: no camera-ray tile culling (A/B, tests)
     bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
     bool env_gather_rgba = false;   // RRTE_GATHER_RGB24=0: gather slabs always RGBA8
+    bool env_gather_inplace = true; // RRTE_GATHER_INPLACE=0: the root's batch share through the send slab
     uint32_t env_guard_leaves = 2;  // RRTE_CSG_GUARDS: 0 = off, N = smallest guarded operand (leaves)
     bool env_wg256 = false;           // RRTE_WG64=0: specialised kernels in 256-thread workgroups (A/B only)
     int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
@@ -208,7 +177,7 @@ struct rrte_ctx {
 };
 
 static rrte_status flush_batch(rrte_ctx* c);
-static rrte_status render_batch(rrte_ctx* c);
+static rrte_status render_batch(rrte_ctx* c, bool at_flush);
 static rrte_status wait_bounded(rrte_ctx* c);
 
 namespace {
@@ -590,7 +559,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         // the open batch's frames render the cached scene: launch them before the scene changes.  Local
         // only (no gather): a rank's own preview render with another scene must not close a batch the
         // other ranks keep open
-        rrte_status r = render_batch(c);
+        rrte_status r = render_batch(c, false);
         if (r != RRTE_OK) return r;
     }
     *upload_ms = 0.0;
@@ -709,9 +678,6 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     mat4_srt(trs, m);
     to_affine12(m, fc.cam_xf);
     k.debug = c->env_debug;  // RRTE_DEBUG ablation bits (profiling only)
-    k.band_done = c->pipe_sig.done;
-    k.band_blocks = c->pipe_sig.blocks;
-    k.band_release = c->env_band_release;
     return k;
 }
 
@@ -1016,189 +982,6 @@ rrte_status finish_frame(rrte_ctx* c) {
     return RRTE_OK;
 }
 
-// The band copy of the blocking path (rrte_ctx::boundary_pipe): workgroup (band, part) waits until the
-// render has counted every workgroup of `band` done, copies its part of the band to the pinned stage
-// (16-byte stores, consecutive lanes consecutive addresses) and publishes it with a system-scope flag
-// (`gen`, or ~0u if the band did not complete within 2 s -- the host then fails the call).
-__global__ __launch_bounds__(256) void band_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                        size_t bytes, size_t band_bytes, uint32_t parts,
-                                                        const uint32_t* band_done, uint32_t per_band,
-                                                        uint32_t last_band, uint32_t* flags, uint32_t gen) {
-    const uint32_t band = blockIdx.x / parts, part = blockIdx.x - band * parts;
-    const uint32_t want = band + 1u == gridDim.x / parts ? last_band : per_band;
-    __shared__ uint32_t ok;
-    if (threadIdx.x == 0) {
-        // the band's kBandShards counters (ray_kernels.hpp), polled every ~1 us
-        const uint32_t* cnt = band_done + (size_t)band * kBandShards * kBandStride;
-        const uint64_t t0 = wall_clock64();
-        uint32_t v = 0;
-        for (;;) {
-            v = 0;
-            for (uint32_t k = 0; k < kBandShards; ++k)
-                v += __hip_atomic_load(cnt + k * kBandStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (v >= want || wall_clock64() - t0 >= 200000000ull) break;  // 2 s of the 100 MHz clock
-            __builtin_amdgcn_s_sleep(40);
-        }
-        ok = v >= want ? 1u : 0u;
-    }
-    __syncthreads();
-    if (ok) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once per wave, after the relaxed polling
-        const size_t b0 = (size_t)band * band_bytes, b1 = b0 + band_bytes < bytes ? b0 + band_bytes : bytes;
-        const size_t per = ((b1 - b0) / parts + 15u) & ~(size_t)15u;
-        const size_t a = b0 + per * part < b1 ? b0 + per * part : b1, e = a + per < b1 ? a + per : b1;
-        const size_t n16 = (e - a) / 16u;
-        const uint4* s4 = reinterpret_cast<const uint4*>(src + a);
-        uint4* d4 = reinterpret_cast<uint4*>(dst + a);
-        for (size_t i = threadIdx.x; i < n16; i += blockDim.x) d4[i] = s4[i];
-        if (threadIdx.x < ((e - a) & 15u)) dst[a + n16 * 16u + threadIdx.x] = src[a + n16 * 16u + threadIdx.x];
-    }
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0)
-        __hip_atomic_store(flags + blockIdx.x, ok ? gen : ~0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// One host thread's share of the copies into the caller's buffer: slice `part` of `parts` of every
-// band, bands in whatever order their flags appear.  Thread 0 also watches the copy kernel: once it has
-// ended, a flag still unset means the frame failed.
-static void copy_share(rrte_ctx::CopyJob& j, int part, int parts) {
-    uint64_t done[2] = {0, 0};  // <= 128 bands
-    uint32_t left = j.nbands;
-    uint64_t spins = 0;
-    while (left && !j.failed.load(std::memory_order_relaxed)) {
-        bool progressed = false;
-        for (uint32_t k = 0; k < j.nbands; ++k) {
-            if ((done[k >> 6] >> (k & 63)) & 1u) continue;
-            bool ready = true;
-            for (uint32_t q = 0; q < rrte_ctx::kCopyParts && ready; ++q) {
-                const uint32_t f = __atomic_load_n(j.flags + k * rrte_ctx::kCopyParts + q, __ATOMIC_ACQUIRE);
-                if (f == ~0u) {
-                    j.failed.store(true, std::memory_order_relaxed);
-                    return;
-                }
-                ready = f == j.flag_gen;
-            }
-            if (!ready) continue;
-            const size_t b0 = (size_t)k * j.band_bytes, b1 = std::min(j.bytes, b0 + j.band_bytes);
-            const size_t per = ((b1 - b0) / parts + 63) & ~(size_t)63;
-            const size_t a = std::min(b1, b0 + per * part), e = std::min(b1, a + per);
-            if (e > a) memcpy(j.dst + a, j.src + a, e - a);
-            done[k >> 6] |= 1ull << (k & 63);
-            --left;
-            progressed = true;
-        }
-        if (!progressed && part == 0 && (++spins & 1023u) == 0) {
-            const hipError_t q = hipEventQuery(j.copied);
-            if (q != hipErrorNotReady) {
-                // the copy kernel has ended (or failed): whatever is not flagged now never will be
-                bool all = true;
-                for (uint32_t k = 0; k < j.nbands * rrte_ctx::kCopyParts && all; ++k)
-                    all = __atomic_load_n(j.flags + k, __ATOMIC_ACQUIRE) == j.flag_gen;
-                if (q != hipSuccess || !all) j.failed.store(true, std::memory_order_relaxed);
-            }
-        }
-    }
-}
-
-static void copy_helper(rrte_ctx* c, int idx) {
-    rrte_ctx::CopyJob& j = c->job;
-    uint64_t seen = 0;
-    for (;;) {
-        {
-            std::unique_lock<std::mutex> lk(j.mu);
-            j.cv.wait(lk, [&] { return j.quit || j.gen != seen; });
-            if (j.quit) return;
-            seen = j.gen;
-        }
-        copy_share(j, idx + 1, rrte_ctx::kCopyHelpers + 1);
-        j.pending.fetch_sub(1, std::memory_order_acq_rel);
-    }
-}
-
-static size_t band_done_bytes(uint32_t nbands) { return (size_t)nbands * kBandShards * kBandStride * sizeof(uint32_t); }
-
-// Band geometry of the pipelined copy for a frame of `rows` rows: 8-row tile rows per band (bands of
-// >= 32 rows, <= 128 bands).
-static uint32_t pipe_band_blocks(uint32_t rows) {
-    uint32_t blocks = 4;
-    while ((rows + blocks * 8 - 1) / (blocks * 8) > 128) blocks *= 2;
-    return blocks;
-}
-
-// Resources of the pipelined copy (first use, or a larger frame).
-static rrte_status pipe_prepare(rrte_ctx* c, size_t bytes, uint32_t nbands) {
-    if (c->cap_stage < bytes) {
-        if (c->h_stage) HIPCHK(c, hipHostFree(c->h_stage));
-        c->h_stage = nullptr;
-        c->cap_stage = 0;
-        HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), bytes, hipHostMallocMapped));
-        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_stage), c->h_stage, 0));
-        c->cap_stage = bytes;
-    }
-    if (c->cap_bands < nbands) {
-        if (c->h_flags) HIPCHK(c, hipHostFree(c->h_flags));
-        if (c->d_band_done) HIPCHK(c, hipFree(c->d_band_done));
-        c->h_flags = nullptr;
-        c->d_band_done = nullptr;
-        c->cap_bands = 0;
-        const size_t nf = (size_t)nbands * rrte_ctx::kCopyParts;
-        HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_flags), nf * sizeof(uint32_t),
-                                hipHostMallocMapped | hipHostMallocCoherent));
-        memset(c->h_flags, 0, nf * sizeof(uint32_t));
-        HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_flags), c->h_flags, 0));
-        HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&c->d_band_done), band_done_bytes(nbands)));
-        c->cap_bands = nbands;
-    }
-    if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-    if (!c->ev_pre) HIPCHK(c, hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming));
-    if (!c->ev_copied) HIPCHK(c, hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming));
-    if (c->helpers.empty())
-        for (int i = 0; i < rrte_ctx::kCopyHelpers; ++i) c->helpers.emplace_back(copy_helper, c, i);
-    return RRTE_OK;
-}
-
-// After the render launch (with pipe_sig set): the band copy on copy_stream, started behind ev_pre (the
-// band counters' reset), and the host copies; the context stream then waits for the copy kernel.
-static rrte_status pipe_copy(rrte_ctx* c, uint8_t* out, uint32_t width, uint32_t rows, uint32_t band_blocks) {
-    const size_t bytes = (size_t)width * rows * 4;
-    const uint32_t gx = (width + 7) / 8, gy = (rows + 7) / 8;
-    const uint32_t nbands = (gy + band_blocks - 1) / band_blocks;
-    const uint32_t gen = c->pipe_gen = (c->pipe_gen % 0x7FFFFFFFu) + 1u;
-    HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->ev_pre, 0));
-    hipLaunchKernelGGL(band_copy_kernel, dim3(nbands * rrte_ctx::kCopyParts), dim3(256), 0, c->copy_stream,
-                       reinterpret_cast<const uint8_t*>(c->d_rgba), c->d_stage, bytes, (size_t)band_blocks * 8u * width * 4u,
-                       rrte_ctx::kCopyParts, c->d_band_done, gx * band_blocks, gx * (gy - (nbands - 1) * band_blocks),
-                       c->d_flags, gen);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev_copied, c->copy_stream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_copied, 0));  // the next frame's render may overwrite d_rgba
-    rrte_ctx::CopyJob& j = c->job;
-    j.dst = out;
-    j.src = c->h_stage;
-    j.bytes = bytes;
-    j.band_bytes = (size_t)band_blocks * 8u * width * 4u;
-    j.nbands = nbands;
-    j.flags = c->h_flags;
-    j.flag_gen = gen;
-    j.copied = c->ev_copied;
-    j.failed.store(false, std::memory_order_relaxed);
-    j.pending.store(rrte_ctx::kCopyHelpers, std::memory_order_release);
-    {
-        std::lock_guard<std::mutex> lk(j.mu);
-        ++j.gen;
-    }
-    j.cv.notify_all();
-    copy_share(j, 0, rrte_ctx::kCopyHelpers + 1);
-    while (j.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-    if (j.failed.load(std::memory_order_relaxed)) {
-        (void)hipStreamSynchronize(c->copy_stream);
-        return fail(c, RRTE_HIP_ERROR, "blocking render: the frame's band copy did not complete (%s)",
-                    hipGetErrorString(hipEventQuery(c->ev_copied)));
-    }
-    return RRTE_OK;
-}
-
 rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out8,
                           float* outf) {
     rrte_status r = validate(c, s, p);
@@ -1213,18 +996,8 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     const int nr = c->nranks, rk = c->rank;
     c->nranks = 1;
     c->rank = 0;
-    const bool pipe = out8 && !outf && c->boundary_pipe && !c->env_wg256;
-    const uint32_t band_blocks = pipe_band_blocks(p->height);
-    if (pipe) {
-        const uint32_t nbands = ((p->height + 7) / 8 + band_blocks - 1) / band_blocks;
-        if ((r = pipe_prepare(c, npix * 4, nbands)) != RRTE_OK) return r;
-        HIPCHK(c, hipMemsetAsync(c->d_band_done, 0, band_done_bytes(nbands), c->stream));
-        HIPCHK(c, hipEventRecord(c->ev_pre, c->stream));
-        c->pipe_sig = {c->d_band_done, band_blocks};
-    }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     r = launch(c, s, p, p->height, c->d_rgba, outf ? c->d_f32 : nullptr, c->stream);
-    c->pipe_sig = {};
     c->nranks = nr;
     c->rank = rk;
     if (r != RRTE_OK) return r;
@@ -1233,12 +1006,8 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     c->pending_primary = (uint64_t)npix * p->samples_per_pixel;
     c->stats.upload_ms = up;
     c->stats.gather_ms = 0.0;
-    if (pipe) {
-        if ((r = pipe_copy(c, out8, p->width, p->height, band_blocks)) != RRTE_OK) return r;
-    } else {
-        if (out8) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
-        if (outf) HIPCHK(c, hipMemcpyAsync(outf, c->d_f32, npix * 16, hipMemcpyDeviceToHost, c->stream));
-    }
+    if (out8) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
+    if (outf) HIPCHK(c, hipMemcpyAsync(outf, c->d_f32, npix * 16, hipMemcpyDeviceToHost, c->stream));
     if ((r = finish_frame(c)) != RRTE_OK) return r;
     c->stats.frames++;
     return RRTE_OK;
@@ -1302,10 +1071,9 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_DIAG_SKIP")) c->env_diag_skip = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GATHER_RGB24")) c->env_gather_rgba = g[0] == '0';
     c->env_guard_leaves = env_guard_setting();
-    if (const char* g = getenv("RRTE_BOUNDARY_PIPE")) c->boundary_pipe = g[0] != '0';
-    if (const char* g = getenv("RRTE_BAND_RELEASE"); g && *g) c->env_band_release = (uint32_t)strtoul(g, nullptr, 0) % 3u;
     if (const char* g = getenv("RRTE_COMM_TIMEOUT_MS")) c->comm_timeout_ms = std::max<uint32_t>(1u, (uint32_t)strtoul(g, nullptr, 0));
     if (const char* g = getenv("RRTE_FAULT_STALL_GATHER")) c->fault_stall_at = strtoull(g, nullptr, 0);
+    if (const char* g = getenv("RRTE_GATHER_INPLACE")) c->env_gather_inplace = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
@@ -1363,19 +1131,6 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_stall) (void)hipHostFree(c->h_stall);
-    {
-        std::lock_guard<std::mutex> lk(c->job.mu);
-        c->job.quit = true;
-    }
-    c->job.cv.notify_all();
-    for (auto& t : c->helpers) t.join();
-    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
-    if (c->h_stage) (void)hipHostFree(c->h_stage);
-    if (c->h_flags) (void)hipHostFree(c->h_flags);
-    if (c->d_band_done) (void)hipFree(c->d_band_done);
-    if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
-    if (c->ev_copied) (void)hipEventDestroy(c->ev_copied);
-    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     for (hipEvent_t e : c->ev_poll)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1447,7 +1202,7 @@ rrte_status rrte_hip_synchronize(rrte_ctx* c) {
     if (!c) return RRTE_INVALID_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     // local: an open gather batch is rendered but stays open (its gather is collective: rrte_hip_flush)
-    rrte_status r = render_batch(c);
+    rrte_status r = render_batch(c, false);
     if (r != RRTE_OK) return r;
     if ((r = wait_bounded(c)) != RRTE_OK) return r;
     HIPCHK(c, hipDeviceSynchronize());
@@ -1658,11 +1413,16 @@ static rrte_status deinterleave(rrte_ctx* c, hipStream_t st, const uint8_t* gath
 // the slab's render stream, after the work queued on the frames' caller streams.  Local: no
 // collective, so a rank may call it on its own (a scene change through a non-gather entry point,
 // rrte_hip_synchronize) without desynchronising the ranks' gathers.
-static rrte_status render_batch(rrte_ctx* c) {
+static rrte_status render_batch(rrte_ctx* c, bool at_flush) {
     rrte_ctx::Batch& b = c->batch;
     if (b.rendered >= b.n) return RRTE_OK;
     HostSection hs(c);
     const int k = c->bslot;
+    // The root renders a batch that is first rendered at its flush (its frame count final) straight
+    // into its own slot of the receive slab, and the gather runs in place: no self-copy of the root's
+    // share (RRTE_GATHER_INPLACE=0: always through the send slab, A/B)
+    if (b.rendered == 0) b.inplace = at_flush && c->rank == b.root && c->env_gather_inplace;
+    uint8_t* base = b.inplace ? c->d_brecv[k] + (size_t)b.root * ((size_t)b.n * b.slice) : c->d_bsend[k];
     hipStream_t rs = c->render_stream[k];
     // the renders follow the frames' caller streams (scene uploads, the callers' own prior work) and
     // the slab's previous batch (its gather reads the send slab)
@@ -1679,7 +1439,7 @@ static rrte_status render_batch(rrte_ctx* c) {
         memcpy(L.k.cam, b.cam + j0, nf * sizeof(FrameCam));
         L.k.nframes = nf;
         L.k.frame_stride = b.slice;
-        uint8_t* dst = c->d_bsend[k] + (size_t)j0 * b.slice;
+        uint8_t* dst = base + (size_t)j0 * b.slice;
         rrte_status r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, rs);
         if (r != RRTE_OK) return r;
     }
@@ -1795,7 +1555,7 @@ static rrte_status flush_batch(rrte_ctx* c) {
         b.n = b.nsrc = b.rendered = 0;
         return fail(c, RRTE_RCCL_ERROR, "gather batch dropped: %s", c->comm_failed ? c->comm_fail_msg.c_str() : "no communicator");
     }
-    rrte_status r = render_batch(c);
+    rrte_status r = render_batch(c, true);
     if (r != RRTE_OK) return comm_abort(c, ("batch render failed: " + c->err).c_str());
     HostSection hs(c);
     const int k = c->bslot;
@@ -1807,7 +1567,8 @@ static rrte_status flush_batch(rrte_ctx* c) {
         hs.lap(4);
         if ((r = before_collective(c, c->comm_stream)) != RRTE_OK) return r;
         if (!(c->env_diag_skip & 1u))
-            NCCLCHK(c, ncclGather(c->d_bsend[k], c->d_brecv[k], count, ncclUint8, b.root, c->comm, c->comm_stream));
+            NCCLCHK(c, ncclGather(b.inplace ? c->d_brecv[k] + (size_t)b.root * count : c->d_bsend[k], c->d_brecv[k],
+                                  count, ncclUint8, b.root, c->comm, c->comm_stream));
         hs.lap(5);
         if (c->rank == b.root && !(c->env_diag_skip & 2u)) {
             DeinterleaveTargets t{};

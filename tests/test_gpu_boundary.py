@@ -1,10 +1,7 @@
 """The blocking drop-in entry point (rrte_hip_render: Raytracer::render's signature, raytracer.rs:45-89,
-host RGBA8 out) with its pipelined host copy: the render counts finished workgroups per row band, a copy
-kernel running beside it moves each finished band into pinned host memory and flags it, host threads
-copy flagged bands into the caller's buffer (rrte_hip.hip band_copy_kernel / pipe_copy).  Its bytes
-must equal the plain path's (RRTE_BOUNDARY_PIPE=0: render, then one hipMemcpy) and the oracle's, for
-sizes whose rows are and are not a multiple of the 8-row tiles and 32-row bands, at 4K (the band cap),
-into reused and fresh buffers, frame after frame."""
+host RGBA8 out, D2H included): its bytes must equal the device-buffer path's (rrte_hip_render_async +
+a copy) and the oracle's, for sizes whose rows are and are not a multiple of the 8-row tiles, at 4K,
+into reused and fresh buffers, frame after frame, on the specialised and the generic kernels."""
 import ctypes as C
 
 import numpy as np
@@ -25,18 +22,18 @@ def _blocking(ctx, sc, prm, out):
 @pytest.mark.parametrize("name,w,h", [("sdf-showcase", 1920, 1080), ("sdf-showcase", 333, 97),
                                       ("sdf-showcase", 64, 7), ("basic-demo", 640, 480),
                                       ("sdf-showcase", 3840, 2160), ("mesh-demo", 200, 120)])
-def test_pipelined_blocking_render_matches_plain_path(name, w, h, monkeypatch):
+def test_blocking_render_matches_device_path(name, w, h):
+    import torch
     objs, lights, cam, cfg = scenes.SCENES[name](w, h)
     sc = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
-    monkeypatch.setenv("RRTE_BOUNDARY_PIPE", "0")
-    plain = Context(0, jit=abi.JIT_ON)
-    want = _blocking(plain, sc, prm, np.zeros(w * h * 4, np.uint8))
-    plain.close()
-    monkeypatch.setenv("RRTE_BOUNDARY_PIPE", "1")
     ctx = Context(0, jit=abi.JIT_ON)
+    dev = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), dev.data_ptr(), None, None))
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    want = dev.cpu().numpy().view(np.uint8)
     reused = np.full(w * h * 4, 7, np.uint8)
-    for f in range(3):  # reused buffer, frame after frame (flag generations)
+    for f in range(3):  # reused buffer, frame after frame
         got = _blocking(ctx, sc, prm, reused)
         assert np.array_equal(got, want), f"frame {f}: {int((got != want).sum())} bytes differ"
     fresh = _blocking(ctx, sc, prm, np.zeros(w * h * 4, np.uint8))
@@ -49,10 +46,8 @@ def test_pipelined_blocking_render_matches_plain_path(name, w, h, monkeypatch):
     ctx.close()
 
 
-def test_pipelined_blocking_render_generic_kernel_and_size_changes(monkeypatch):
-    """The generic kernel counts bands too; a smaller and a larger frame on one context reuse / regrow
-    the stage and the band flags."""
-    monkeypatch.setenv("RRTE_BOUNDARY_PIPE", "1")
+def test_blocking_render_generic_kernel_and_size_changes():
+    """The generic kernel's blocking frames; smaller and larger frames on one context."""
     ctx = Context(0, jit=abi.JIT_OFF)
     for w, h in [(320, 180), (96, 40), (1280, 720), (320, 180)]:
         objs, lights, cam, cfg = scenes.sdf_showcase(w, h)

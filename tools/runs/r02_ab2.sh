@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of two library builds on the headline (three interleaved rounds) and advanced-demo (two),
-# after a parity subset.  usage: tools/r02_ab2.sh <libA.so> <libB.so> <pytest -k expr>
+# after a parity subset.  usage: tools/runs/r02_ab2.sh <libA.so> <libB.so> <pytest -k expr>
 set -o pipefail
 A=${1:?libA}; B=${2:?libB}; K=${3:?k}
 mkdir -p gpurun_out/ab2

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline A/B of two library builds (three interleaved rounds, default and 20 steps) plus one PMC
-# pass each of VALU / SALU instruction counts.  usage: tools/r02_ab_pmc.sh <libA.so> <libB.so> [parity-k]
+# pass each of VALU / SALU instruction counts.  usage: tools/runs/r02_ab_pmc.sh <libA.so> <libB.so> [parity-k]
 set -o pipefail
 A=${1:?libA}; B=${2:?libB}; K=${3:-}
 R=$GRAFT_REPO_ROOT

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Full check of HEAD on one GPU: GPU suite, smoke, default and 20-step bench, trace + PMC profile.
-# usage: tools/r02_head.sh <tag>
+# usage: tools/runs/r02_head.sh <tag>
 set -o pipefail
 TAG=${1:-head}
 mkdir -p gpurun_out

@@ -5,4 +5,4 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_fpexact.py -x -q --timeout 250 --timeout-method thread -k "sqrt or rcp or detects" > gpurun_out/sqc_fp.log 2>&1 || { echo FPEXACT FAILED; tail -30 gpurun_out/sqc_fp.log; exit 1; }
 tail -1 gpurun_out/sqc_fp.log
-bash tools/r02_ab2.sh ab/libA.so rrte_amd/lib/librrte_hip.so "specialised or 1080p or convex or extra or golden or baseline"
+bash tools/runs/r02_ab2.sh ab/libA.so rrte_amd/lib/librrte_hip.so "specialised or 1080p or convex or extra or golden or baseline"

@@ -15,8 +15,14 @@ for r in rows:
     r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
 rows.sort(key=lambda r: r["s"])
 ray = [r for r in rows if "rrte_jit_kernel" in r["Kernel_Name"] or "ray_kernel" in r["Kernel_Name"]]
+if any(int(r.get("Grid_Size_Z") or 1) > 1 for r in ray):
+    ray = [r for r in ray if int(r.get("Grid_Size_Z") or 1) > 1]  # batched path: the multi-frame launches only
 w0 = ray[-n]["s"]
-win = [r for r in rows if r["s"] >= w0]
+# the window: from the first of those launches to the end of the last kernel that follows the last one
+# before the next launch of another kind of frame (the bench's later single-frame measurements)
+after = [r for r in rows if r["s"] > ray[-1]["s"] and ("rrte_jit_kernel" in r["Kernel_Name"] or "ray_kernel" in r["Kernel_Name"])]
+cut = after[0]["s"] if after else None
+win = [r for r in rows if r["s"] >= w0 and (cut is None or r["s"] < cut)]
 t1 = max(r["e"] for r in win)
 per = defaultdict(list)
 for r in win:
@@ -34,7 +40,7 @@ for s, e in iv:
         cur[1] = max(cur[1], e)
 busy += cur[1] - cur[0]
 span = (t1 - w0) / 1e3
-lines = [f"# {title}", "", f"source: `rocprofv3 --kernel-trace`; window = the last {n} ray-kernel launches "
+lines = [f"# {title}", "", f"source: `rocprofv3 --kernel-trace`; window = the last {n} ray-kernel launches (multi-frame ones when the run has any) "
          f"({frames} frames) and every kernel started after the first of them", "",
          "| kernel | count | mean us | total us |", "|---|---|---|---|"]
 for name, d in sorted(per.items(), key=lambda kv: -sum(kv[1])):
