@@ -315,6 +315,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    t_enq = time.perf_counter()  # host time to enqueue the timed frames (diagnostic: host-bound if close to elapsed)
     if gath:
         ctx.check(lib.rrte_hip_flush(ctx.h))  # the last, partial gather batch
     if spin:
@@ -470,6 +471,7 @@ def main():
         }
         line["primary_only"] = {"value": round(primary / elapsed / 1e6, 3), "unit": "Mray/s"}
         line["frame_latency_ms"] = round(latency_ms, 4)
+        line["host_enqueue_ms_per_step"] = round((t_enq - t0) / args.steps * 1e3, 4)
         line["d2h_ms"] = round(d2h_ms, 4)  # frame to pinned host memory, excluded from `value`
         if pmc and pmc.get("valu") is not None:
             line["valu"] = dict(pmc["valu"])

@@ -89,7 +89,7 @@ struct rrte_ctx {
     // per launch) on the slab's render stream into the send slab, and the comm stream gathers all B
     // frames to the root in ONE ncclGather and de-interleaves them.  Every collective is issued on
     // the one comm stream, in program order; slab k's render stream overlaps slab k-1's gather.
-    static constexpr int kMaxBatch = 16, kBatchSlabs = 3;
+    static constexpr int kMaxBatch = 16, kBatchSlabs = 6;
     static_assert(kMaxBatch == sizeof(rrte::DeinterleaveTargets::full) / sizeof(uint32_t*), "batch targets");
     uint32_t gather_batch = 1;
     hipStream_t comm_stream = nullptr;
@@ -110,6 +110,8 @@ struct rrte_ctx {
         hipEvent_t ev_src[kMaxBatch] = {};   // recorded on src[i] at the flush
     } batch;
     int bslot = 0;
+    int batch_slabs = 3;                     // slabs in the ring (RRTE_BATCH_SLABS, A/B: 1..kBatchSlabs; 3 measured
+                                             // best against 4 and 6, tools/runs/r03_call16.sh)
     hipEvent_t ev_batch[kBatchSlabs] = {};   // the slab's last batch gathered and de-interleaved
     hipEvent_t ev_render[kBatchSlabs] = {};  // the slab's last batch rendered
     uint8_t* d_bsend[kBatchSlabs] = {};
@@ -124,7 +126,7 @@ struct rrte_ctx {
     bool comm_failed = false;
     std::string comm_fail_msg;
     uint64_t gathers_issued = 0;       // collectives issued on this communicator (both forms)
-    hipEvent_t ev_poll[3 + 3] = {};    // bounded waits: the context's streams + the last gather
+    hipEvent_t ev_poll[3 + kBatchSlabs] = {};  // bounded waits: the context's streams + the last gather
     // RRTE_FAULT_STALL_GATHER=N (fault injection, tests only): the N-th collective on this context is
     // preceded on its stream by a kernel that spins until the host releases it (or 5 s pass) -- a
     // stalled peer as seen from this rank.
@@ -1073,6 +1075,8 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     c->env_guard_leaves = env_guard_setting();
     if (const char* g = getenv("RRTE_COMM_TIMEOUT_MS")) c->comm_timeout_ms = std::max<uint32_t>(1u, (uint32_t)strtoul(g, nullptr, 0));
     if (const char* g = getenv("RRTE_FAULT_STALL_GATHER")) c->fault_stall_at = strtoull(g, nullptr, 0);
+    if (const char* g = getenv("RRTE_BATCH_SLABS"); g && *g)
+        c->batch_slabs = std::max(1, std::min(rrte_ctx::kBatchSlabs, (int)strtol(g, nullptr, 0)));
     if (const char* g = getenv("RRTE_GATHER_INPLACE")) c->env_gather_inplace = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
@@ -1503,11 +1507,12 @@ static rrte_status comm_abort(rrte_ctx* c, const char* why) {
 // communicator exists, ncclCommGetAsyncError) instead of blocking, so a gather that never completes
 // -- a dead or stalled peer -- surfaces as RRTE_RCCL_ERROR after comm_timeout_ms instead of a hang.
 static rrte_status wait_bounded(rrte_ctx* c) {
-    hipStream_t ss[6] = {c->stream, c->comm_stream, c->render_stream[0], c->render_stream[1], c->render_stream[2],
-                         c->last_gather_stream};
-    static_assert(sizeof(c->ev_poll) / sizeof(c->ev_poll[0]) == 6, "poll events");
+    constexpr int kPoll = 3 + rrte_ctx::kBatchSlabs;
+    static_assert(sizeof(c->ev_poll) / sizeof(c->ev_poll[0]) == kPoll, "poll events");
+    hipStream_t ss[kPoll] = {c->stream, c->comm_stream, c->last_gather_stream};
+    for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i) ss[3 + i] = c->render_stream[i];
     int n = 0;
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < kPoll; ++i) {
         if (!ss[i]) continue;
         if (!c->ev_poll[n]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_poll[n], hipEventDisableTiming));
         HIPCHK(c, hipEventRecord(c->ev_poll[n], ss[i]));
@@ -1584,7 +1589,7 @@ static rrte_status flush_batch(rrte_ctx* c) {
     if ((r = issue()) != RRTE_OK) return comm_abort(c, ("batch gather failed: " + c->err).c_str());
     c->last_gather_stream = c->comm_stream;
     c->last_gather_ev = c->ev_batch[k];
-    c->bslot = (k + 1) % rrte_ctx::kBatchSlabs;
+    c->bslot = (k + 1) % c->batch_slabs;
     b.n = b.nsrc = b.rendered = 0;
     hs.lap(7);
     return RRTE_OK;
@@ -1657,9 +1662,12 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             // every rank holds a receive slab too (the root's is the only one written)
             const size_t send = (size_t)b.cap * slice, recv = send * (size_t)c->nranks;
             if (c->cap_bsend[k] < send || c->cap_brecv[k] < recv) {
-                HIPCHK(c, hipDeviceSynchronize());  // no render or gather may still use the slab being resized
-                if ((r = ensure(c, c->d_bsend[k], c->cap_bsend[k], send)) != RRTE_OK) return r;
-                if ((r = ensure(c, c->d_brecv[k], c->cap_brecv[k], recv)) != RRTE_OK) return r;
+                // every slab of the ring at once (one device sync at the first batch, none in steady state)
+                HIPCHK(c, hipDeviceSynchronize());  // no render or gather may still use a slab being resized
+                for (int q = 0; q < rrte_ctx::kBatchSlabs; ++q) {
+                    if ((r = ensure(c, c->d_bsend[q], c->cap_bsend[q], send)) != RRTE_OK) return r;
+                    if ((r = ensure(c, c->d_brecv[q], c->cap_brecv[q], recv)) != RRTE_OK) return r;
+                }
             }
         }
         hs.lap(2);
