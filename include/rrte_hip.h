@@ -263,7 +263,7 @@ typedef struct rrte_stats {
     double upload_ms;        /* scene H2D time (0 when the scene was cached)   */
     uint64_t frames;         /* frames rendered by this context                */
     uint32_t jit_active;     /* last frame's kernel: 0 generic, 1 full, 2 topology specialisation */
-    uint32_t _pad0;
+    uint32_t hot_tiles;      /* tiles the last launch dispatched first (hot-first tile order; 0: image order) */
     double jit_compile_ms;   /* hiprtc compile time of the last specialised kernel */
 } rrte_stats;
 

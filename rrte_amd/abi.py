@@ -102,7 +102,7 @@ class SceneIR(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("primary_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("kernel_ms", C.c_double),
                 ("gather_ms", C.c_double), ("upload_ms", C.c_double), ("frames", C.c_uint64),
-                ("jit_active", C.c_uint32), ("_pad0", C.c_uint32), ("jit_compile_ms", C.c_double)]
+                ("jit_active", C.c_uint32), ("hot_tiles", C.c_uint32), ("jit_compile_ms", C.c_double)]
 
 
 assert C.sizeof(Prim) == 192 and C.sizeof(Material) == 32 and C.sizeof(Light) == 80

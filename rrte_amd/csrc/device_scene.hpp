@@ -77,6 +77,10 @@ struct FrameCam {
 // cameras (blockIdx.z = frame; batched multi-GPU frames, rrte_hip_set_gather_batch).
 constexpr uint32_t kMaxLaunchFrames = 8;
 
+// Hot-first tile order (KParams::hot): at most this many tiles, packed x | y << 16, and tile rows
+// < 32 * kHotRowWords (4096 pixels) per launch.
+constexpr uint32_t kMaxHotTiles = 256, kHotRowWords = 16;
+
 // Per-launch constants, passed by value (kernel arguments land in SGPRs).
 struct KParams {
     uint32_t width, height;
@@ -93,8 +97,19 @@ struct KParams {
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
     uint32_t nframes;        // frames of this launch (gridDim.z), cam[0 .. nframes)
     uint64_t frame_stride;   // bytes between consecutive frames' RGBA8 / slab outputs
+    // Tile order of 64-thread-workgroup launches: grid (tiles_x, nframes, hot_rows + tile rows).
+    // Workgroup rows [0, hot_rows) render the hot tiles hot[0 .. hot_n) of every frame first -- the
+    // tiles the context measured slowest on an earlier frame (rrte_hip.hip, TileProfile) -- and the
+    // image-order workgroup of a hot tile exits (its row has a bit in hot_row_bits).  Pixels are
+    // independent (raytracer.rs:57-60), so any order renders the same bytes; this one starts the
+    // frame's longest waves first instead of wherever image order puts them.
+    uint32_t* tile_cost;     // non-null: frame 0's workgroups store their duration (100 MHz ticks) at [y * tiles_x + x]
+    uint32_t tiles_x, hot_rows, hot_n;
+    uint32_t hot_row_bits[kHotRowWords];
+    uint32_t hot[kMaxHotTiles];
     FrameCam cam[kMaxLaunchFrames];
 };
+static_assert(sizeof(KParams) <= 3584, "kernel arguments stay below the 4 KB kernarg limit");
 
 // Internal KParams::flags bit (never in the public rrte_render_params::flags): the launch writes
 // a gather slab of packed RGB24 pixels (3 B, alpha dropped) instead of RGBA8.  The host sets it

@@ -1917,13 +1917,14 @@ __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
 // SALU ops and a scalar load each).  Call with all 64 lanes active.  The host enables it only when
 // a tile's local rows are consecutive image rows (no band mapping, or bands of a multiple of the
 // tile height).
-__device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp, const FrameCam& cm) {
+__device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp, const FrameCam& cm, uint32_t tx,
+                                                     uint32_t ty) {
     const uint32_t sh = cm.tile_cull;
     if (!sh) return ~0u;
     uint32_t bx, by;
     if (kWg64) {  // one 8x8 tile per workgroup
-        bx = (blockIdx.x * 8u) >> sh;
-        by = image_row(kp, blockIdx.y * 8u) >> sh;
+        bx = (tx * 8u) >> sh;
+        by = image_row(kp, ty * 8u) >> sh;
     } else {
         const uint32_t wave = sh == 3u ? (threadIdx.x >> 6) : 0u;
         bx = (blockIdx.x * 16u + (wave & 1u) * 8u) >> sh;
@@ -1939,6 +1940,33 @@ __device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp, const Fr
     return m | (cm.tile_n < 32u ? (~0u << cm.tile_n) : 0u);  // objects past the table: never culled
 }
 
+// The tile (x, y in workgroup units) and frame of this workgroup (KParams::hot, hot-first order);
+// run = false for an unused hot slot and for the image-order workgroup of a hot tile.
+struct LaunchTile { uint32_t x, y, z; bool run; };
+__device__ __forceinline__ LaunchTile launch_tile(const KParams& kp) {
+    if (!kWg64) return LaunchTile{blockIdx.x, blockIdx.y, blockIdx.z, true};
+    LaunchTile t{blockIdx.x, 0u, blockIdx.y, true};
+    const uint32_t r = blockIdx.z;
+    if (r < kp.hot_rows) {  // hot slot k: wave-uniform index, a scalar load
+        const uint32_t k = r * kp.tiles_x + blockIdx.x;
+        t.run = k < kp.hot_n;
+        const uint32_t h = kp.hot[t.run ? k : 0u];
+        t.x = h & 0xffffu;
+        t.y = h >> 16;
+        return t;
+    }
+    t.y = r - kp.hot_rows;
+    if ((kp.hot_row_bits[(t.y >> 5) & (kHotRowWords - 1u)] >> (t.y & 31u)) & 1u) {
+        // a row with hot tiles: is this one of them?  lane j tests hot[j], hot[j + 64], ...
+        const uint32_t me = t.x | (t.y << 16), lane = threadIdx.x & 63u;
+        bool dup = false;
+        for (uint32_t i = 0; i < kp.hot_n; i += 64u)
+            if (i + lane < kp.hot_n && kp.hot[i + lane] == me) dup = true;
+        t.run = __ballot(dup) == 0ull;
+    }
+    return t;
+}
+
 // One lane per pixel; wave = workgroup = 8x8 tile (RRTE_WG256: 16x16-pixel workgroups).  Every lane
 // of a wave runs the sample loop (lanes past the image edge are idle but
 // present) so the culling reductions see converged waves.  CULL selects the
@@ -1948,18 +1976,22 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
                                                 uint32_t* __restrict__ out_rgba8, float4* __restrict__ out_f32,
                                                 unsigned long long* __restrict__ counters) {
     const uint32_t lane = threadIdx.x & 63u, wave = kWg64 ? 0u : threadIdx.x >> 6;
-    // frame blockIdx.z of the launch: its camera, its output (multi-frame launches have no f32 output)
-    const FrameCam& cm = kp.cam[blockIdx.z];
-    if (out_rgba8 && blockIdx.z)
-        out_rgba8 = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out_rgba8) + blockIdx.z * kp.frame_stride);
+    const LaunchTile tile = launch_tile(kp);
+    if (!tile.run) return;
+    // frame tile.z of the launch: its camera, its output (multi-frame launches have no f32 output)
+    const FrameCam& cm = kp.cam[tile.z];
+    if (out_rgba8 && tile.z)
+        out_rgba8 = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out_rgba8) + tile.z * kp.frame_stride);
     // RRTE_DEBUG bit 4 (diagnostics, tools/wave_times.py): per-wave start / duration from the 100 MHz
     // wall clock into the f32 buffer instead of colours
     const bool stamps = (kp.debug & 16u) && out_f32;
+    const uint32_t tiles_x = kWg64 ? kp.tiles_x : gridDim.x;
     // bit 5: only workgroup (debug >> 16) runs (its waves' durations alone on the GPU)
-    const uint32_t brow = blockIdx.y;
-    if ((kp.debug & 32u) && brow * gridDim.x + blockIdx.x != (kp.debug >> 16)) return;
-    const uint64_t t_wave0 = stamps ? wall_clock64() : 0ull;
-    const uint32_t x = kWg64 ? blockIdx.x * 8u + (lane & 7u) : blockIdx.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t brow = tile.y;
+    if ((kp.debug & 32u) && brow * tiles_x + tile.x != (kp.debug >> 16)) return;
+    const bool timed = stamps || (kp.tile_cost && tile.z == 0u);
+    const uint64_t t_wave0 = timed ? wall_clock64() : 0ull;
+    const uint32_t x = kWg64 ? tile.x * 8u + (lane & 7u) : tile.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t lr = kWg64 ? brow * 8u + (lane >> 3) : brow * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool live = x < kp.width && lr < kp.rows;
     const uint32_t xc = live ? x : 0u;
@@ -1968,7 +2000,7 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     uint32_t nshadow = 0;
     Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
     const uint32_t nsamples = SINGLE ? 1u : kp.spp;
-    const uint32_t pmask = camera_tile_mask(kp, cm);
+    const uint32_t pmask = camera_tile_mask(kp, cm, tile.x, tile.y);
     // camera ray of sample s (raytracer.rs:66-70): per-(pixel, sample) RNG stream, jitter, generate_ray
     auto camera_ray = [&](uint32_t s, uint32_t& st) {
         st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
@@ -2075,13 +2107,15 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
         // 256 counter shards, one 128-B line each: same-address atomics from
         // every wave of the grid would serialise at the memory side.
         if (lane == 0 && v) {
-            const uint32_t shard = (blockIdx.x + blockIdx.y * gridDim.x + threadIdx.x / 64u * 61u) & (kCounterShards - 1u);
+            const uint32_t shard = (tile.x + tile.y * tiles_x + threadIdx.x / 64u * 61u) & (kCounterShards - 1u);
             atomicAdd(counters + shard * kCounterStride, (unsigned long long)v);
         }
     }
+    if (kWg64 && kp.tile_cost && tile.z == 0u && lane == 0)  // tile profile (TileProfile, rrte_hip.hip)
+        kp.tile_cost[brow * tiles_x + tile.x] = (uint32_t)(wall_clock64() - t_wave0);
     if (stamps && lane == 0) {
         const uint64_t t1 = wall_clock64();
-        const uint32_t wid = (brow * gridDim.x + blockIdx.x) * 4u + wave;
+        const uint32_t wid = (brow * tiles_x + tile.x) * 4u + wave;
         uint32_t* s = reinterpret_cast<uint32_t*>(out_f32) + 4u * wid;
         s[0] = (uint32_t)t_wave0;
         s[1] = (uint32_t)(t_wave0 >> 32);

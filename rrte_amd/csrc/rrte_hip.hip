@@ -176,6 +176,35 @@ struct rrte_ctx {
                                  // de-interleave, 4 no comm-stream waits -- results are wrong
     double hp[10] = {};
     uint64_t hp_frames = 0;
+    // Hot-first tile order (KParams::hot).  Every kTileReprofile-th launch of one launch shape (size,
+    // rows, band mapping, mode, kernel) times each tile of its frame 0 on the device and copies the
+    // durations back asynchronously; once they have arrived, later launches of that shape dispatch its
+    // slowest tiles first.  The order never changes a pixel, only when each tile starts.
+    // RRTE_TILE_ORDER=0 turns it off (A/B, tests).
+    struct TileProfile {
+        std::string key;                 // launch shape the hot list belongs to
+        std::string pending_key;         // shape of the profile in flight
+        bool pending = false;
+        hipEvent_t ev = nullptr;         // the profile's D2H copy done
+        uint32_t* d_cost = nullptr; size_t cap_d = 0;
+        uint32_t* h_cost = nullptr; size_t cap_h = 0;  // pinned
+        uint32_t tiles = 0, tiles_x = 0;                 // of the pending profile
+        std::vector<uint32_t> hot;       // packed x | y << 16, image order
+        uint32_t row_bits[kHotRowWords] = {};
+        uint64_t launches = 0;           // launches of `key` since its last profile
+        uint64_t profiles = 0;           // completed profiles (rrte_stats-like counter for tests)
+    } tprof;
+    bool env_tile_order = true;
+    bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
+    // camera-ray tile rectangles of the last camera (fill_tile_rects)
+    struct {
+        bool valid = false;
+        uint64_t gen = 0;
+        uint32_t width = 0, height = 0, band = 0;
+        rrte_camera cam{};
+        uint32_t tile_cull = 0, tile_n = 0;
+        uint32_t rect[32] = {};
+    } tile_rect_cache;
 };
 
 static rrte_status flush_batch(rrte_ctx* c);
@@ -694,7 +723,33 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
 // (inside the pixel).  A sphere that contains the eye or reaches the plane z = 0 keeps the whole
 // frame.  Bit-identical results by construction: a skipped test is one every lane would miss
 // (tests/test_gpu_parity.py test_camera_tile_culling_is_exact).
-void fill_tile_rects(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& kk) {
+void fill_tile_rects_uncached(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& kk);
+
+// The rectangles depend only on the camera, the frame size, the band height and the cached scene's
+// bounds: frames of an unchanged camera reuse the last result (the double-precision trigonometry is
+// most of a frame call's host time in the batched multi-GPU path).
+void fill_tile_rects(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& kk) {
+    auto& tc = c->tile_rect_cache;
+    if (tc.valid && tc.gen == c->scene_gen && tc.width == p->width && tc.height == p->height &&
+        tc.band == kk.band_rows && !memcmp(&tc.cam, &s->camera, sizeof tc.cam)) {
+        kk.cam[0].tile_cull = tc.tile_cull;
+        kk.cam[0].tile_n = tc.tile_n;
+        memcpy(kk.cam[0].tile_rect, tc.rect, sizeof tc.rect);
+        return;
+    }
+    fill_tile_rects_uncached(c, s, p, kk);
+    tc.valid = true;
+    tc.gen = c->scene_gen;
+    tc.width = p->width;
+    tc.height = p->height;
+    tc.band = kk.band_rows;
+    tc.cam = s->camera;
+    tc.tile_cull = kk.cam[0].tile_cull;
+    tc.tile_n = kk.cam[0].tile_n;
+    memcpy(tc.rect, kk.cam[0].tile_rect, sizeof tc.rect);
+}
+
+void fill_tile_rects_uncached(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& kk) {
     FrameCam& k = kk.cam[0];
     const uint32_t band_rows = kk.band_rows;
     k.tile_cull = 0;
@@ -907,7 +962,7 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
     return k;
 }
 
-LaunchPlan plan_launch(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
+LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
                        uint32_t internal_flags) {
     LaunchPlan L;
     L.k = make_params(c, s, p, rows);
@@ -926,13 +981,129 @@ LaunchPlan plan_launch(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_ren
     return L;
 }
 
+// Hot-first tile order (rrte_ctx::TileProfile, KParams::hot).
+constexpr uint64_t kTileReprofile = 64;  // launches of one shape between two profiles
+
+// The hot list from a completed profile: the slowest tiles, at most kMaxHotTiles, each at least
+// twice the mean tile time and a quarter of the slowest, in image order (packed x | y << 16).
+void build_hot_list(rrte_ctx::TileProfile& tp) {
+    const uint32_t n = tp.tiles;
+    tp.hot.clear();
+    memset(tp.row_bits, 0, sizeof tp.row_bits);
+    if (n == 0 || tp.tiles_x == 0) return;
+    double sum = 0.0;
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        sum += tp.h_cost[i];
+        mx = std::max(mx, tp.h_cost[i]);
+    }
+    const double thr = std::max(2.0 * sum / n, 0.25 * mx);
+    std::vector<uint32_t> idx(n);
+    for (uint32_t i = 0; i < n; ++i) idx[i] = i;
+    const uint32_t k = std::min<uint32_t>(n, kMaxHotTiles);
+    std::partial_sort(idx.begin(), idx.begin() + k, idx.end(),
+                      [&](uint32_t a, uint32_t b) { return tp.h_cost[a] > tp.h_cost[b] || (tp.h_cost[a] == tp.h_cost[b] && a < b); });
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint32_t i = idx[j];
+        if ((double)tp.h_cost[i] < thr) break;
+        const uint32_t x = i % tp.tiles_x, y = i / tp.tiles_x;
+        tp.hot.push_back(x | (y << 16));
+        tp.row_bits[y >> 5] |= 1u << (y & 31u);
+    }
+    std::sort(tp.hot.begin(), tp.hot.end());
+}
+
+// Sets the plan's tile order (hot list, tile profile) for a launch of kernel `kern`; true when this
+// launch is profiled (the caller copies the durations back after it).
+bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern) {
+    KParams& k = L.k;
+    k.tiles_x = L.gx;
+    k.hot_rows = k.hot_n = 0;
+    k.tile_cost = nullptr;
+    memset(k.hot_row_bits, 0, sizeof k.hot_row_bits);
+    if (!c->env_tile_order || c->env_wg256 || L.gy > 32u * kHotRowWords || L.gx > 0xffffu || (k.debug & 48u))
+        return false;
+    auto& tp = c->tprof;
+    std::string key(reinterpret_cast<const char*>(&kern), sizeof kern);
+    const uint32_t shape[] = {k.width, k.height, k.rows, k.row0, k.band_rows, k.nranks, k.rank, k.spp, k.max_depth,
+                              (uint32_t)L.mode, (uint32_t)L.cull, (uint32_t)L.single};
+    key.append(reinterpret_cast<const char*>(shape), sizeof shape);
+    if (tp.pending && hipEventQuery(tp.ev) == hipSuccess) {
+        tp.pending = false;
+        if (tp.pending_key == key) {
+            build_hot_list(tp);
+            tp.key = key;
+            tp.launches = 0;
+            ++tp.profiles;
+        }
+    }
+    if (tp.key != key) {  // another shape: drop the list, profile as soon as the copy buffer is free
+        tp.key = key;
+        tp.hot.clear();
+        memset(tp.row_bits, 0, sizeof tp.row_bits);
+        tp.launches = kTileReprofile;
+        if (c->env_tile_order_fixed) {
+            // RRTE_TILE_ORDER=2 (tests): a fixed list of kMaxHotTiles tiles spread over the frame, first and
+            // last tile included, from the first launch on; no profiling
+            const uint32_t n = L.gx * L.gy, m = std::min<uint32_t>(n, kMaxHotTiles);
+            for (uint32_t j = 0; j < m; ++j) {
+                const uint32_t i = m > 1 ? (uint32_t)((uint64_t)j * (n - 1) / (m - 1)) : 0u;
+                const uint32_t x = i % L.gx, y = i / L.gx;
+                tp.hot.push_back(x | (y << 16));
+                tp.row_bits[y >> 5] |= 1u << (y & 31u);
+            }
+            std::sort(tp.hot.begin(), tp.hot.end());
+            tp.launches = 0;
+        }
+    }
+    if (c->env_tile_order_fixed) tp.launches = 0;
+    const bool profile = !tp.pending && tp.launches >= kTileReprofile;
+    ++tp.launches;
+    if (!tp.hot.empty()) {
+        k.hot_n = (uint32_t)tp.hot.size();
+        k.hot_rows = (k.hot_n + L.gx - 1) / L.gx;
+        memcpy(k.hot, tp.hot.data(), k.hot_n * sizeof(uint32_t));
+        memcpy(k.hot_row_bits, tp.row_bits, sizeof tp.row_bits);
+    }
+    if (!profile) return false;
+    const size_t n = (size_t)L.gx * L.gy;
+    if (ensure(c, tp.d_cost, tp.cap_d, n) != RRTE_OK) return false;
+    if (tp.cap_h < n) {
+        if (tp.h_cost) (void)hipHostFree(tp.h_cost);
+        tp.h_cost = nullptr;
+        tp.cap_h = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_cost), n * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+            return false;
+        tp.cap_h = n;
+    }
+    if (!tp.ev && hipEventCreateWithFlags(&tp.ev, hipEventDisableTiming) != hipSuccess) return false;
+    k.tile_cost = tp.d_cost;
+    tp.pending_key = key;
+    tp.tiles = (uint32_t)n;
+    tp.tiles_x = L.gx;
+    return true;
+}
+
+// Queues the profiled launch's copy-back on its stream (plan_tile_order returned true).
+rrte_status finish_tile_profile(rrte_ctx* c, const LaunchPlan& L, hipStream_t st) {
+    auto& tp = c->tprof;
+    HIPCHK(c, hipMemcpyAsync(tp.h_cost, tp.d_cost, (size_t)tp.tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipEventRecord(tp.ev, st));
+    tp.pending = true;
+    (void)L;
+    return RRTE_OK;
+}
+
 // Launch plan `L` (L.k.nframes frames) on `st`; the cached scene is the plan's.
 rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     if (L.gy == 0) return RRTE_OK;
     Cull cl{L.cull ? c->d_bounds : nullptr, L.num_prims};
-    const dim3 grid(L.gx, L.gy, L.k.nframes), block(kBlockThreads);
     JitKernel* jk = jit_kernel_for(c, L.mode, L.cull, L.single);
     c->stats.jit_active = jk ? (jk->topology ? 2u : 1u) : 0u;
+    // 64-thread workgroups: (tile column, frame, hot rows + tile rows), KParams::hot
+    const bool profile = plan_tile_order(c, L, jk ? (const void*)jk->fn : nullptr);
+    c->stats.hot_tiles = L.k.hot_n;
+    const dim3 grid(L.gx, L.k.nframes, L.k.hot_rows + L.gy), block(kBlockThreads);
     if (jk) {
         unsigned long long* ctr = c->d_counters;
         MeshView mv = c->mesh_view;
@@ -940,12 +1111,12 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         void* args[] = {&L.k, &cl, &mv, &d_rgba, &d_f32, &ctr, &vals};
         HostSection hs(c);
         if (c->env_wg256)
-            HIPCHK(c, hipModuleLaunchKernel(jk->fn, (L.k.width + 15) / 16, (L.k.rows + 15) / 16, grid.z, 256, 1, 1, 0,
-                                            st, args, nullptr));
+            HIPCHK(c, hipModuleLaunchKernel(jk->fn, (L.k.width + 15) / 16, (L.k.rows + 15) / 16, L.k.nframes, 256, 1, 1,
+                                            0, st, args, nullptr));
         else
             HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, st, args, nullptr));
         hs.lap(8);
-        return RRTE_OK;
+        return profile ? finish_tile_profile(c, L, st) : RRTE_OK;
     }
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
                  c->mesh_view};
@@ -957,7 +1128,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     else
         hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     HIPCHK(c, hipGetLastError());
-    return RRTE_OK;
+    return profile ? finish_tile_profile(c, L, st) : RRTE_OK;
 }
 
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
@@ -1079,6 +1250,10 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         c->batch_slabs = std::max(1, std::min(rrte_ctx::kBatchSlabs, (int)strtol(g, nullptr, 0)));
     if (const char* g = getenv("RRTE_GATHER_INPLACE")) c->env_gather_inplace = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
+    if (const char* g = getenv("RRTE_TILE_ORDER")) {
+        c->env_tile_order = g[0] != '0';
+        c->env_tile_order_fixed = g[0] == '2';
+    }
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
@@ -1135,6 +1310,9 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_stall) (void)hipHostFree(c->h_stall);
+    if (c->tprof.d_cost) (void)hipFree(c->tprof.d_cost);
+    if (c->tprof.h_cost) (void)hipHostFree(c->tprof.h_cost);
+    if (c->tprof.ev) (void)hipEventDestroy(c->tprof.ev);
     for (hipEvent_t e : c->ev_poll)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);

@@ -1,0 +1,158 @@
+"""Hot-first tile order (KParams::hot, rrte_hip.hip plan_tile_order): a launch may dispatch a list of
+tiles first and skip them in image order.  Pixels are independent (raytracer.rs:57-60), so every
+order must give the same bytes, linear floats and shadow-ray counts as image order.
+RRTE_TILE_ORDER=2 forces a fixed list of 256 tiles spread over the frame (first and last tile
+included) on every launch, so these tests run the hot slots, the partial hot row and the
+image-order skip on every kernel kind, mode and launch shape; RRTE_TILE_ORDER=0 is image order; the
+default measures the tiles on a profiled launch and uses the measured list once its copy arrives."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from rrte_amd import LoweredScene, abi, scenes
+from rrte_amd.math import vec3
+from rrte_amd.renderer import Context
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(monkeypatch, order, jit, **env):
+    monkeypatch.setenv("RRTE_TILE_ORDER", order)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ctx = Context(0, jit=jit)
+    monkeypatch.delenv("RRTE_TILE_ORDER")
+    for k in env:
+        monkeypatch.delenv(k)
+    return ctx
+
+
+def _render(ctx, sc, prm, rows=None):
+    """(RGBA8 bytes, linear floats, shadow rays, hot tiles) of one frame through render_async."""
+    import torch
+    rows = prm.height if rows is None else rows
+    p = abi.RenderParams.from_buffer_copy(prm)
+    rgba = torch.full((rows * p.width,), -1, dtype=torch.int32, device="cuda")
+    ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(p), rgba.data_ptr(), None, None))
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    s1 = ctx.stats()
+    p.flags |= abi.FLAG_F32_LINEAR
+    f32 = torch.zeros(rows * p.width * 4, dtype=torch.float32, device="cuda")
+    ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(p), None, f32.data_ptr(), None))
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    return (rgba.cpu().numpy().view(np.uint8), f32.cpu().numpy().view(np.uint32), s1.shadow_rays, s1.hot_tiles)
+
+
+CASES = [("sdf-showcase", 320, 200, "lambert_shadow", 1), ("sdf-showcase", 162, 90, "lambert_shadow", 1),
+         ("advanced-demo", 200, 120, "lambert_shadow", 1), ("sdf-showcase", 96, 64, "refcompat", 3),
+         ("deformation-stress", 64, 40, "lambert_shadow", 1), ("mesh-demo", 160, 96, "lambert_shadow", 1)]
+
+
+@pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
+@pytest.mark.parametrize("name,w,h,mode,spp", CASES)
+def test_fixed_hot_list_is_exact(name, w, h, mode, spp, jit, monkeypatch):
+    objs, lights, cam, cfg = scenes.SCENES[name](w, h, mode=mode)
+    if spp > 1:
+        cfg.samples_per_pixel, cfg.max_depth, cfg.jitter = spp, 5, "random"
+    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    ref = _ctx(monkeypatch, "0", jit)
+    hot = _ctx(monkeypatch, "2", jit)
+    a, b = _render(ref, sc, prm), _render(hot, sc, prm)
+    tiles = ((w + 7) // 8) * ((h + 7) // 8)
+    assert a[3] == 0 and b[3] == min(256, tiles)
+    assert np.array_equal(a[0], b[0]), (a[0] != b[0]).sum()
+    assert np.array_equal(a[1], b[1])
+    assert a[2] == b[2]
+    ref.close()
+    hot.close()
+
+
+@pytest.mark.parametrize("nranks,rank", [(3, 1), (8, 0), (8, 7)])
+def test_fixed_hot_list_on_band_mapped_ranks(nranks, rank, monkeypatch):
+    """One rank's packed interleaved bands (RRTE_EMULATE_RANK): hot tiles address the rank's local
+    tile rows, the camera-tile mask maps them to image rows."""
+    w, h, band = 256, 200, 16
+    objs, lights, cam, cfg = scenes.sdf_showcase(w, h)
+    cfg.band_rows = band
+    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    rows = abi.load().rrte_hip_band_rows_for_rank(h, band, nranks, rank)
+    env = {"RRTE_EMULATE_RANK": f"{nranks}:{rank}"}
+    ref = _ctx(monkeypatch, "0", abi.JIT_ON, **env)
+    hot = _ctx(monkeypatch, "2", abi.JIT_ON, **env)
+    a, b = _render(ref, sc, prm, rows), _render(hot, sc, prm, rows)
+    assert b[3] > 0
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+    ref.close()
+    hot.close()
+
+
+def test_fixed_hot_list_at_4k(monkeypatch):
+    """BASELINE configs[3]'s size: 480 x 270 tiles (270 tile rows: the row bitmap's upper words) and
+    16x16 camera-culling blocks."""
+    objs, lights, cam, cfg = scenes.sdf_showcase(3840, 2160)
+    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    ref = _ctx(monkeypatch, "0", abi.JIT_ON)
+    hot = _ctx(monkeypatch, "2", abi.JIT_ON)
+    a, b = _render(ref, sc, prm), _render(hot, sc, prm)
+    assert b[3] == 256
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+    ref.close()
+    hot.close()
+
+
+def test_measured_hot_list(monkeypatch):
+    """The default policy: the first launch of a shape is profiled, the durations come back
+    asynchronously and a later launch dispatches the measured slowest tiles first; every frame on
+    the way is identical to image order."""
+    objs, lights, cam, cfg = scenes.sdf_showcase(640, 360)
+    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    ref = _ctx(monkeypatch, "0", abi.JIT_ON)
+    want = _render(ref, sc, prm)
+    ref.close()
+    monkeypatch.delenv("RRTE_TILE_ORDER", raising=False)
+    ctx = Context(0, jit=abi.JIT_ON)
+    seen = 0
+    for _ in range(6):
+        got = _render(ctx, sc, prm)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[2]
+        seen = max(seen, got[3])
+    assert 0 < seen <= 256
+    ctx.close()
+
+
+def test_fixed_hot_list_in_batched_gathers(monkeypatch):
+    """Multi-frame launches of the batched gather path (blockIdx.y = frame): every frame's hot tiles
+    first, 8 frames per launch, a partial last batch."""
+    import torch
+    frames = []
+    for i in range(11):
+        objs, lights, cam, cfg = scenes.sdf_showcase(320, 200)
+        cam.transform.position = vec3(0.7 * i, 8.0 - 0.3 * i, 20.0)
+        cam.look_at((0, 2, 0))
+        frames.append((LoweredScene(objs, lights, cam), cfg.lower()))
+    ref = _ctx(monkeypatch, "0", abi.JIT_ON)
+    want = []
+    for sc, prm in frames:
+        buf = np.zeros(prm.width * prm.height * 4, dtype=np.uint8)
+        ref.check(ref.lib.rrte_hip_render(ref.h, sc.ref(), C.byref(prm), buf.ctypes.data_as(C.POINTER(C.c_uint8))))
+        want.append(buf)
+    ref.close()
+    ctx = _ctx(monkeypatch, "2", abi.JIT_ON, RRTE_FORCE_GATHER="1")
+    lib = ctx.lib
+    uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+    ctx.check(lib.rrte_hip_comm_unique_id(uid))
+    ctx.check(lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
+    ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 8))
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = [torch.full((p.width * p.height,), -1, dtype=torch.int32, device="cuda") for _, p in frames]
+    for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
+        ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
+                                                    C.c_void_p(streams[i % 2].cuda_stream)))
+    ctx.check(lib.rrte_hip_flush(ctx.h))
+    ctx.check(lib.rrte_hip_synchronize(ctx.h))
+    assert ctx.stats().hot_tiles == 256
+    for i, o in enumerate(outs):
+        got = o.cpu().numpy().view(np.uint8)
+        assert np.array_equal(got, want[i]), f"frame {i}: {(got != want[i]).sum()} bytes differ"
+    ctx.close()
