@@ -77,9 +77,18 @@ struct FrameCam {
 // cameras (blockIdx.z = frame; batched multi-GPU frames, rrte_hip_set_gather_batch).
 constexpr uint32_t kMaxLaunchFrames = 8;
 
-// Hot-first tile order (KParams::hot): at most this many tiles, packed x | y << 16, and tile rows
-// < 32 * kHotRowWords (4096 pixels) per launch.
-constexpr uint32_t kMaxHotTiles = 256, kHotRowWords = 16;
+// Hot-first tile order (KParams::hot): at most this many hot slots, and tile rows < 32 * kHotRowWords
+// (4096 pixels) per launch.  A slot is packed y << 16 | x << 4 | (parts - 1) << 2 | part (x < 4096):
+// a split tile (parts > 1, at most 4) takes `parts` consecutive slots, each rendering the tile's
+// camera rays and the shadow rays of the lights KParams::light_part gives that part.
+constexpr uint32_t kMaxHotTiles = 256, kHotRowWords = 16, kMaxSplitLights = 64;
+__host__ __device__ constexpr uint32_t hot_pack(uint32_t x, uint32_t y, uint32_t part, uint32_t parts) {
+    return (y << 16) | (x << 4) | ((parts - 1u) << 2) | part;
+}
+__host__ __device__ constexpr uint32_t hot_x(uint32_t h) { return (h >> 4) & 0xfffu; }
+__host__ __device__ constexpr uint32_t hot_y(uint32_t h) { return h >> 16; }
+__host__ __device__ constexpr uint32_t hot_part(uint32_t h) { return h & 3u; }
+__host__ __device__ constexpr uint32_t hot_parts(uint32_t h) { return ((h >> 2) & 3u) + 1u; }
 
 // Per-launch constants, passed by value (kernel arguments land in SGPRs).
 struct KParams {
@@ -104,6 +113,13 @@ struct KParams {
     // independent (raytracer.rs:57-60), so any order renders the same bytes; this one starts the
     // frame's longest waves first instead of wherever image order puts them.
     uint32_t* tile_cost;     // non-null: frame 0's workgroups store their duration (100 MHz ticks) at [y * tiles_x + x]
+    // Split hot tiles (LAMBERT_SHADOW, one sample): each part publishes its lights' terms for every
+    // lane into xterms (block (first slot * nframes + frame) of num_lights * 3 * 64 floats) and counts
+    // itself in xcount; the last part to arrive sums every light's term in light order -- the
+    // reference's accumulation order (raytracer.rs ray_color) -- and writes the pixels.
+    float* xterms;
+    uint32_t* xcount;
+    uint32_t light_part[kMaxSplitLights / 16];  // 2 bits per light: the part that shades it
     uint32_t tiles_x, hot_rows, hot_n;
     uint32_t hot_row_bits[kHotRowWords];
     uint32_t hot[kMaxHotTiles];

@@ -189,11 +189,29 @@ struct rrte_ctx {
         uint32_t* d_cost = nullptr; size_t cap_d = 0;
         uint32_t* h_cost = nullptr; size_t cap_h = 0;  // pinned
         uint32_t tiles = 0, tiles_x = 0;                 // of the pending profile
-        std::vector<uint32_t> hot;       // packed x | y << 16, image order
+        // the measured slowest tiles, slowest first (tile index, 100 MHz ticks), and the slot list
+        // composed from them for `slots_parts` parts per split tile
+        std::vector<std::pair<uint32_t, uint32_t>> top;
+        uint32_t top_max = 0;
+        bool fixed = false;              // RRTE_TILE_ORDER=2 list
+        std::vector<uint32_t> slots;     // packed hot_pack slots, ascending
+        uint32_t slots_parts = 0;
         uint32_t row_bits[kHotRowWords] = {};
         uint64_t launches = 0;           // launches of `key` since its last profile
-        uint64_t profiles = 0;           // completed profiles (rrte_stats-like counter for tests)
+        uint64_t profiles = 0;           // completed profiles
     } tprof;
+    // Exchange areas of split tiles (KParams::xterms / xcount), one per launch in a ring; an area is
+    // reused after the launch that last used it has completed (else the new launch waits for it)
+    struct XArea {
+        float* terms = nullptr; size_t cap_terms = 0;
+        uint32_t* count = nullptr; size_t cap_count = 0;  // zero between uses (the last part resets)
+        hipEvent_t ev = nullptr;
+        bool used = false;
+    };
+    static constexpr int kXAreas = 8;
+    XArea xarea[kXAreas];
+    int xnext = 0;
+    bool env_tile_split = true;        // RRTE_TILE_SPLIT=0: hot tiles are never split (A/B)
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
@@ -984,12 +1002,14 @@ LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_pa
 // Hot-first tile order (rrte_ctx::TileProfile, KParams::hot).
 constexpr uint64_t kTileReprofile = 64;  // launches of one shape between two profiles
 
-// The hot list from a completed profile: the slowest tiles, at most kMaxHotTiles, each at least
-// twice the mean tile time and a quarter of the slowest, in image order (packed x | y << 16).
+// The slowest tiles of a completed profile: at most kMaxHotTiles, each at least twice the mean tile
+// time and a quarter of the slowest, slowest first.
 void build_hot_list(rrte_ctx::TileProfile& tp) {
     const uint32_t n = tp.tiles;
-    tp.hot.clear();
-    memset(tp.row_bits, 0, sizeof tp.row_bits);
+    tp.top.clear();
+    tp.slots.clear();
+    tp.slots_parts = 0;
+    tp.fixed = false;
     if (n == 0 || tp.tiles_x == 0) return;
     double sum = 0.0;
     uint32_t mx = 0;
@@ -1003,31 +1023,74 @@ void build_hot_list(rrte_ctx::TileProfile& tp) {
     const uint32_t k = std::min<uint32_t>(n, kMaxHotTiles);
     std::partial_sort(idx.begin(), idx.begin() + k, idx.end(),
                       [&](uint32_t a, uint32_t b) { return tp.h_cost[a] > tp.h_cost[b] || (tp.h_cost[a] == tp.h_cost[b] && a < b); });
-    for (uint32_t j = 0; j < k; ++j) {
-        const uint32_t i = idx[j];
-        if ((double)tp.h_cost[i] < thr) break;
-        const uint32_t x = i % tp.tiles_x, y = i / tp.tiles_x;
-        tp.hot.push_back(x | (y << 16));
-        tp.row_bits[y >> 5] |= 1u << (y & 31u);
-    }
-    std::sort(tp.hot.begin(), tp.hot.end());
+    for (uint32_t j = 0; j < k && (double)tp.h_cost[idx[j]] >= thr; ++j) tp.top.emplace_back(idx[j], tp.h_cost[idx[j]]);
+    tp.top_max = mx;
 }
 
-// Sets the plan's tile order (hot list, tile profile) for a launch of kernel `kern`; true when this
+// Split tiles: a hot tile at least this fraction of the slowest one is rendered as one part per
+// shadow-casting light (at most 4), so its lights' shadow marches run on different waves at once.
+constexpr double kSplitFrac = 0.5;
+
+// Hot slots for `parts` parts per split tile (1: no splitting), ascending.
+void compose_slots(rrte_ctx::TileProfile& tp, uint32_t parts, uint32_t tiles_x, uint32_t tiles) {
+    tp.slots.clear();
+    memset(tp.row_bits, 0, sizeof tp.row_bits);
+    tp.slots_parts = parts;
+    auto add = [&](uint32_t i, uint32_t np) {
+        const uint32_t x = i % tiles_x, y = i / tiles_x;
+        for (uint32_t q = 0; q < np; ++q) tp.slots.push_back(hot_pack(x, y, q, np));
+        tp.row_bits[y >> 5] |= 1u << (y & 31u);
+    };
+    if (tp.fixed) {
+        // RRTE_TILE_ORDER=2 (tests): tiles spread over the frame, first and last included, every other
+        // one split when splitting is possible; as many as fit in kMaxHotTiles slots
+        uint32_t m = std::min<uint32_t>(tiles, kMaxHotTiles);
+        while (m > 1 && (m + 1) / 2 * parts + m / 2 > kMaxHotTiles) --m;
+        for (uint32_t j = 0; j < m; ++j) add(m > 1 ? (uint32_t)((uint64_t)j * (tiles - 1) / (m - 1)) : 0u, j % 2 ? 1u : parts);
+    } else {
+        for (const auto& t : tp.top) {
+            const uint32_t np = parts > 1 && t.second >= kSplitFrac * tp.top_max ? parts : 1u;
+            if (tp.slots.size() + np > kMaxHotTiles) break;
+            add(t.first, np);
+        }
+    }
+    std::sort(tp.slots.begin(), tp.slots.end());
+}
+
+// Parts of a split tile for this launch (1: no splitting): LAMBERT_SHADOW frames of one sample whose
+// scene has at least two shadow-casting lights (one part each, at most 4; ambient lights go to part 0).
+uint32_t split_parts(const rrte_ctx* c, const LaunchPlan& L, uint32_t light_part[kMaxSplitLights / 16]) {
+    memset(light_part, 0, sizeof(uint32_t) * (kMaxSplitLights / 16));
+    if (!c->env_tile_split || L.mode != RRTE_MODE_LAMBERT_SHADOW || L.k.spp != 1 || L.k.max_depth == 0 ||
+        L.num_lights > kMaxSplitLights || c->h_lights.size() < L.num_lights)
+        return 1;
+    uint32_t casters = 0;
+    for (uint32_t i = 0; i < L.num_lights; ++i) casters += c->h_lights[i].kind != RRTE_LIGHT_AMBIENT;
+    const uint32_t parts = std::min<uint32_t>(casters, 4u);
+    if (parts < 2) return 1;
+    for (uint32_t i = 0, q = 0; i < L.num_lights; ++i)
+        if (c->h_lights[i].kind != RRTE_LIGHT_AMBIENT) light_part[i >> 4] |= ((q++ % parts) & 3u) << ((i & 15u) * 2u);
+    return parts;
+}
+
+// Sets the plan's tile order (hot slots, tile profile) for a launch of kernel `kern`; true when this
 // launch is profiled (the caller copies the durations back after it).
-bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern) {
+bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t st) {
     KParams& k = L.k;
     k.tiles_x = L.gx;
     k.hot_rows = k.hot_n = 0;
     k.tile_cost = nullptr;
+    k.xterms = nullptr;
+    k.xcount = nullptr;
     memset(k.hot_row_bits, 0, sizeof k.hot_row_bits);
-    if (!c->env_tile_order || c->env_wg256 || L.gy > 32u * kHotRowWords || L.gx > 0xffffu || (k.debug & 48u))
+    if (!c->env_tile_order || c->env_wg256 || L.gy > 32u * kHotRowWords || L.gx > 0xfffu || (k.debug & 48u))
         return false;
     auto& tp = c->tprof;
     std::string key(reinterpret_cast<const char*>(&kern), sizeof kern);
     const uint32_t shape[] = {k.width, k.height, k.rows, k.row0, k.band_rows, k.nranks, k.rank, k.spp, k.max_depth,
                               (uint32_t)L.mode, (uint32_t)L.cull, (uint32_t)L.single};
     key.append(reinterpret_cast<const char*>(shape), sizeof shape);
+    const uint32_t tiles = L.gx * L.gy;
     if (tp.pending && hipEventQuery(tp.ev) == hipSuccess) {
         tp.pending = false;
         if (tp.pending_key == key) {
@@ -1039,58 +1102,81 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern) {
     }
     if (tp.key != key) {  // another shape: drop the list, profile as soon as the copy buffer is free
         tp.key = key;
-        tp.hot.clear();
-        memset(tp.row_bits, 0, sizeof tp.row_bits);
+        tp.top.clear();
+        tp.slots.clear();
+        tp.slots_parts = 0;
+        tp.fixed = c->env_tile_order_fixed;
         tp.launches = kTileReprofile;
-        if (c->env_tile_order_fixed) {
-            // RRTE_TILE_ORDER=2 (tests): a fixed list of kMaxHotTiles tiles spread over the frame, first and
-            // last tile included, from the first launch on; no profiling
-            const uint32_t n = L.gx * L.gy, m = std::min<uint32_t>(n, kMaxHotTiles);
-            for (uint32_t j = 0; j < m; ++j) {
-                const uint32_t i = m > 1 ? (uint32_t)((uint64_t)j * (n - 1) / (m - 1)) : 0u;
-                const uint32_t x = i % L.gx, y = i / L.gx;
-                tp.hot.push_back(x | (y << 16));
-                tp.row_bits[y >> 5] |= 1u << (y & 31u);
-            }
-            std::sort(tp.hot.begin(), tp.hot.end());
-            tp.launches = 0;
-        }
     }
-    if (c->env_tile_order_fixed) tp.launches = 0;
+    if (tp.fixed) tp.launches = 0;  // RRTE_TILE_ORDER=2: the fixed list, never profiled
     const bool profile = !tp.pending && tp.launches >= kTileReprofile;
     ++tp.launches;
-    if (!tp.hot.empty()) {
-        k.hot_n = (uint32_t)tp.hot.size();
+    const uint32_t parts = split_parts(c, L, k.light_part);
+    if ((!tp.top.empty() || tp.fixed) && (tp.slots_parts != parts || tp.slots.empty())) compose_slots(tp, parts, L.gx, tiles);
+    if (!tp.slots.empty()) {
+        k.hot_n = (uint32_t)tp.slots.size();
         k.hot_rows = (k.hot_n + L.gx - 1) / L.gx;
-        memcpy(k.hot, tp.hot.data(), k.hot_n * sizeof(uint32_t));
+        memcpy(k.hot, tp.slots.data(), k.hot_n * sizeof(uint32_t));
         memcpy(k.hot_row_bits, tp.row_bits, sizeof tp.row_bits);
     }
     if (!profile) return false;
-    const size_t n = (size_t)L.gx * L.gy;
-    if (ensure(c, tp.d_cost, tp.cap_d, n) != RRTE_OK) return false;
-    if (tp.cap_h < n) {
+    if (ensure(c, tp.d_cost, tp.cap_d, tiles) != RRTE_OK) return false;
+    if (tp.cap_h < tiles) {
         if (tp.h_cost) (void)hipHostFree(tp.h_cost);
         tp.h_cost = nullptr;
         tp.cap_h = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_cost), n * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_cost), tiles * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
             return false;
-        tp.cap_h = n;
+        tp.cap_h = tiles;
     }
     if (!tp.ev && hipEventCreateWithFlags(&tp.ev, hipEventDisableTiming) != hipSuccess) return false;
+    if (hipMemsetAsync(tp.d_cost, 0, tiles * sizeof(uint32_t), st) != hipSuccess) return false;  // atomicMax per tile
     k.tile_cost = tp.d_cost;
     tp.pending_key = key;
-    tp.tiles = (uint32_t)n;
+    tp.tiles = tiles;
     tp.tiles_x = L.gx;
     return true;
 }
 
-// Queues the profiled launch's copy-back on its stream (plan_tile_order returned true).
-rrte_status finish_tile_profile(rrte_ctx* c, const LaunchPlan& L, hipStream_t st) {
+// The exchange area of a launch with split tiles (KParams::xterms / xcount); nullptr-free on success.
+rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& area) {
+    area = -1;
+    KParams& k = L.k;
+    bool any = false;
+    for (uint32_t i = 0; i < k.hot_n && !any; ++i) any = hot_parts(k.hot[i]) > 1;
+    if (!any) return RRTE_OK;
+    area = c->xnext;
+    c->xnext = (c->xnext + 1) % rrte_ctx::kXAreas;
+    auto& xa = c->xarea[area];
+    const size_t groups = (size_t)k.hot_n * k.nframes;
+    const size_t terms = groups * k.num_lights * 3u * 64u;
+    if (xa.cap_terms < terms || xa.cap_count < groups) {
+        HIPCHK(c, hipDeviceSynchronize());  // no launch may still use the area being resized (first use)
+        rrte_status r;
+        if ((r = ensure(c, xa.terms, xa.cap_terms, terms)) != RRTE_OK) return r;
+        if ((r = ensure(c, xa.count, xa.cap_count, groups)) != RRTE_OK) return r;
+        HIPCHK(c, hipMemset(xa.count, 0, xa.cap_count * sizeof(uint32_t)));
+        xa.used = false;
+    }
+    if (!xa.ev) HIPCHK(c, hipEventCreateWithFlags(&xa.ev, hipEventDisableTiming));
+    if (xa.used && hipEventQuery(xa.ev) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(st, xa.ev, 0));
+    k.xterms = xa.terms;
+    k.xcount = xa.count;
+    return RRTE_OK;
+}
+
+// Queues the profiled launch's copy-back on its stream (plan_tile_order returned true) and marks the
+// launch's split exchange area busy until the launch completes.
+rrte_status finish_tile_order(rrte_ctx* c, bool profile, int area, hipStream_t st) {
+    if (area >= 0) {
+        HIPCHK(c, hipEventRecord(c->xarea[area].ev, st));
+        c->xarea[area].used = true;
+    }
+    if (!profile) return RRTE_OK;
     auto& tp = c->tprof;
     HIPCHK(c, hipMemcpyAsync(tp.h_cost, tp.d_cost, (size_t)tp.tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipEventRecord(tp.ev, st));
     tp.pending = true;
-    (void)L;
     return RRTE_OK;
 }
 
@@ -1101,7 +1187,9 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     JitKernel* jk = jit_kernel_for(c, L.mode, L.cull, L.single);
     c->stats.jit_active = jk ? (jk->topology ? 2u : 1u) : 0u;
     // 64-thread workgroups: (tile column, frame, hot rows + tile rows), KParams::hot
-    const bool profile = plan_tile_order(c, L, jk ? (const void*)jk->fn : nullptr);
+    const bool profile = plan_tile_order(c, L, jk ? (const void*)jk->fn : nullptr, st);
+    int area = -1;
+    if (rrte_status r = plan_split_area(c, L, st, area); r != RRTE_OK) return r;
     c->stats.hot_tiles = L.k.hot_n;
     const dim3 grid(L.gx, L.k.nframes, L.k.hot_rows + L.gy), block(kBlockThreads);
     if (jk) {
@@ -1116,7 +1204,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         else
             HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, st, args, nullptr));
         hs.lap(8);
-        return profile ? finish_tile_profile(c, L, st) : RRTE_OK;
+        return finish_tile_order(c, profile, area, st);
     }
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
                  c->mesh_view};
@@ -1128,7 +1216,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     else
         hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     HIPCHK(c, hipGetLastError());
-    return profile ? finish_tile_profile(c, L, st) : RRTE_OK;
+    return finish_tile_order(c, profile, area, st);
 }
 
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
@@ -1254,6 +1342,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         c->env_tile_order = g[0] != '0';
         c->env_tile_order_fixed = g[0] == '2';
     }
+    if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] != '0';
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
@@ -1313,6 +1402,11 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->tprof.d_cost) (void)hipFree(c->tprof.d_cost);
     if (c->tprof.h_cost) (void)hipHostFree(c->tprof.h_cost);
     if (c->tprof.ev) (void)hipEventDestroy(c->tprof.ev);
+    for (auto& xa : c->xarea) {
+        if (xa.terms) (void)hipFree(xa.terms);
+        if (xa.count) (void)hipFree(xa.count);
+        if (xa.ev) (void)hipEventDestroy(xa.ev);
+    }
     for (hipEvent_t e : c->ev_poll)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);

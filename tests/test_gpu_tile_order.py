@@ -1,9 +1,12 @@
-"""Hot-first tile order (KParams::hot, rrte_hip.hip plan_tile_order): a launch may dispatch a list of
-tiles first and skip them in image order.  Pixels are independent (raytracer.rs:57-60), so every
-order must give the same bytes, linear floats and shadow-ray counts as image order.
-RRTE_TILE_ORDER=2 forces a fixed list of 256 tiles spread over the frame (first and last tile
-included) on every launch, so these tests run the hot slots, the partial hot row and the
-image-order skip on every kernel kind, mode and launch shape; RRTE_TILE_ORDER=0 is image order; the
+"""Hot-first tile order and split hot tiles (KParams::hot, rrte_hip.hip plan_tile_order): a launch
+may dispatch a list of tiles first and skip them in image order, and a hot tile may be rendered as
+one workgroup per shadow-casting light, the last of which sums the lights' terms in light order.
+Pixels are independent (raytracer.rs:57-60) and adding a light that contributes nothing as +0 is
+exact, so every order and split must give the same bytes, linear floats and shadow-ray counts as
+image order.  RRTE_TILE_ORDER=2 forces a fixed list of tiles spread over the frame (first and last
+tile included, every other one split where splitting applies) on every launch, so these tests run
+the hot slots, split parts, the partial hot row and the image-order skip on every kernel kind, mode
+and launch shape; RRTE_TILE_ORDER=0 is image order, RRTE_TILE_SPLIT=0 hot order without splits; the
 default measures the tiles on a profiled launch and uses the measured list once its copy arrives."""
 import ctypes as C
 
@@ -13,6 +16,8 @@ import pytest
 from rrte_amd import LoweredScene, abi, scenes
 from rrte_amd.math import vec3
 from rrte_amd.renderer import Context
+
+import scenes_extra as se  # noqa: E402  (tests/ is on sys.path, as for test_gpu_parity)
 
 pytestmark = pytest.mark.gpu
 
@@ -44,28 +49,45 @@ def _render(ctx, sc, prm, rows=None):
     return (rgba.cpu().numpy().view(np.uint8), f32.cpu().numpy().view(np.uint32), s1.shadow_rays, s1.hot_tiles)
 
 
+def _fixed_slots(tiles, parts):
+    """Slots of RRTE_TILE_ORDER=2's list (rrte_hip.hip compose_slots): m tiles, every other one split."""
+    m = min(tiles, 256)
+    while m > 1 and (m + 1) // 2 * parts + m // 2 > 256:
+        m -= 1
+    return (m + 1) // 2 * parts + m // 2
+
+
+SCENES = dict(scenes.SCENES, **{"all-lights": se.all_lights_scene, "mixed": se.mixed_scene})
+# (scene, W, H, mode, spp): 3 lights (3 parts), 5 point lights (4 parts, round robin), point +
+# directional + spot + ambient (3 parts, ambient in part 0), odd sizes, REFCOMPAT (never split)
 CASES = [("sdf-showcase", 320, 200, "lambert_shadow", 1), ("sdf-showcase", 162, 90, "lambert_shadow", 1),
-         ("advanced-demo", 200, 120, "lambert_shadow", 1), ("sdf-showcase", 96, 64, "refcompat", 3),
+         ("advanced-demo", 200, 120, "lambert_shadow", 1), ("all-lights", 120, 72, "lambert_shadow", 1),
+         ("mixed", 96, 64, "lambert_shadow", 1), ("sdf-showcase", 96, 64, "refcompat", 3),
          ("deformation-stress", 64, 40, "lambert_shadow", 1), ("mesh-demo", 160, 96, "lambert_shadow", 1)]
 
 
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
 @pytest.mark.parametrize("name,w,h,mode,spp", CASES)
 def test_fixed_hot_list_is_exact(name, w, h, mode, spp, jit, monkeypatch):
-    objs, lights, cam, cfg = scenes.SCENES[name](w, h, mode=mode)
+    objs, lights, cam, cfg = SCENES[name](w, h, mode=mode)
     if spp > 1:
         cfg.samples_per_pixel, cfg.max_depth, cfg.jitter = spp, 5, "random"
     sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
     ref = _ctx(monkeypatch, "0", jit)
-    hot = _ctx(monkeypatch, "2", jit)
-    a, b = _render(ref, sc, prm), _render(hot, sc, prm)
+    a = _render(ref, sc, prm)
+    assert a[3] == 0
     tiles = ((w + 7) // 8) * ((h + 7) // 8)
-    assert a[3] == 0 and b[3] == min(256, tiles)
-    assert np.array_equal(a[0], b[0]), (a[0] != b[0]).sum()
-    assert np.array_equal(a[1], b[1])
-    assert a[2] == b[2]
+    casters = sum(1 for lt in sc.lights[:sc.ir.num_lights] if lt.kind != abi.LIGHT_AMBIENT)
+    for split in ("0", "1"):
+        hot = _ctx(monkeypatch, "2", jit, RRTE_TILE_SPLIT=split)
+        b = _render(hot, sc, prm)
+        parts = min(casters, 4) if split == "1" and mode == "lambert_shadow" and spp == 1 else 1
+        assert b[3] == _fixed_slots(tiles, parts if parts > 1 else 1)
+        assert np.array_equal(a[0], b[0]), (split, (a[0] != b[0]).sum())
+        assert np.array_equal(a[1], b[1]), split
+        assert a[2] == b[2], split
+        hot.close()
     ref.close()
-    hot.close()
 
 
 @pytest.mark.parametrize("nranks,rank", [(3, 1), (8, 0), (8, 7)])
@@ -95,7 +117,7 @@ def test_fixed_hot_list_at_4k(monkeypatch):
     ref = _ctx(monkeypatch, "0", abi.JIT_ON)
     hot = _ctx(monkeypatch, "2", abi.JIT_ON)
     a, b = _render(ref, sc, prm), _render(hot, sc, prm)
-    assert b[3] == 256
+    assert b[3] == 256  # 3 lights: 64 split tiles of 3 parts + 64 whole ones
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
     ref.close()
     hot.close()
@@ -151,7 +173,7 @@ def test_fixed_hot_list_in_batched_gathers(monkeypatch):
                                                     C.c_void_p(streams[i % 2].cuda_stream)))
     ctx.check(lib.rrte_hip_flush(ctx.h))
     ctx.check(lib.rrte_hip_synchronize(ctx.h))
-    assert ctx.stats().hot_tiles == 256
+    assert ctx.stats().hot_tiles == 256  # per launch: 64 split tiles x 3 parts + 64 whole tiles
     for i, o in enumerate(outs):
         got = o.cpu().numpy().view(np.uint8)
         assert np.array_equal(got, want[i]), f"frame {i}: {(got != want[i]).sum()} bytes differ"
