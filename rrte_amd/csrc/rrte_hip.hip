@@ -1151,12 +1151,24 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
     const size_t groups = (size_t)k.hot_n * k.nframes;
     const size_t terms = groups * k.num_lights * 3u * 64u;
     if (xa.cap_terms < terms || xa.cap_count < groups) {
-        HIPCHK(c, hipDeviceSynchronize());  // no launch may still use the area being resized (first use)
-        rrte_status r;
-        if ((r = ensure(c, xa.terms, xa.cap_terms, terms)) != RRTE_OK) return r;
-        if ((r = ensure(c, xa.count, xa.cap_count, groups)) != RRTE_OK) return r;
-        HIPCHK(c, hipMemset(xa.count, 0, xa.cap_count * sizeof(uint32_t)));
-        xa.used = false;
+        // every area of the ring at once, uncached (the kernel's exchange relies on it), sized for the
+        // largest launch (kMaxHotTiles slots x kMaxLaunchFrames frames) of this light count: one device
+        // synchronisation at the first split launch, none later
+        HIPCHK(c, hipDeviceSynchronize());
+        const size_t gmax = (size_t)kMaxHotTiles * kMaxLaunchFrames, tmax = gmax * k.num_lights * 3u * 64u;
+        for (auto& a : c->xarea) {
+            if (a.terms) (void)hipFree(a.terms);
+            if (a.count) (void)hipFree(a.count);
+            a.terms = nullptr;
+            a.count = nullptr;
+            a.cap_terms = a.cap_count = 0;
+            HIPCHK(c, hipExtMallocWithFlags(reinterpret_cast<void**>(&a.terms), tmax * sizeof(float), hipDeviceMallocUncached));
+            HIPCHK(c, hipExtMallocWithFlags(reinterpret_cast<void**>(&a.count), gmax * sizeof(uint32_t), hipDeviceMallocUncached));
+            HIPCHK(c, hipMemset(a.count, 0, gmax * sizeof(uint32_t)));
+            a.cap_terms = tmax;
+            a.cap_count = gmax;
+            a.used = false;
+        }
     }
     if (!xa.ev) HIPCHK(c, hipEventCreateWithFlags(&xa.ev, hipEventDisableTiming));
     if (xa.used && hipEventQuery(xa.ev) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(st, xa.ev, 0));
