@@ -74,14 +74,17 @@ struct FrameCam {
 };
 
 // A launch renders up to kMaxLaunchFrames frames of one scene with the same parameters and their own
-// cameras (blockIdx.z = frame; batched multi-GPU frames, rrte_hip_set_gather_batch).
+// cameras (blockIdx.y = frame; batched multi-GPU frames, rrte_hip_set_gather_batch).
 constexpr uint32_t kMaxLaunchFrames = 8;
 
 // Hot-first tile order (KParams::hot): at most this many hot slots, and tile rows < 32 * kHotRowWords
 // (4096 pixels) per launch.  A slot is packed y << 16 | x << 4 | (parts - 1) << 2 | part (x < 4096):
 // a split tile (parts > 1, at most 4) takes `parts` consecutive slots, each rendering the tile's
 // camera rays and the shadow rays of the lights KParams::light_part gives that part.
-constexpr uint32_t kMaxHotTiles = 256, kHotRowWords = 16, kMaxSplitLights = 64;
+// The slots live in device memory (KParams::hot): kMaxHotTiles slots, then kHotRows + 1 tile-row
+// offsets (the slots of tile row y are [off[y], off[y + 1])).
+constexpr uint32_t kMaxHotTiles = 1024, kHotRowWords = 16, kHotRows = 32 * kHotRowWords, kMaxSplitLights = 64;
+constexpr uint32_t kHotListWords = kMaxHotTiles + kHotRows + 1;
 __host__ __device__ constexpr uint32_t hot_pack(uint32_t x, uint32_t y, uint32_t part, uint32_t parts) {
     return (y << 16) | (x << 4) | ((parts - 1u) << 2) | part;
 }
@@ -104,10 +107,10 @@ struct KParams {
     float bg[4];
     float t_min, bias, inv_gamma, inv_spp;
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
-    uint32_t nframes;        // frames of this launch (gridDim.z), cam[0 .. nframes)
+    uint32_t nframes;        // frames of this launch (gridDim.y), cam[0 .. nframes)
     uint64_t frame_stride;   // bytes between consecutive frames' RGBA8 / slab outputs
     // Tile order of 64-thread-workgroup launches: grid (tiles_x, nframes, hot_rows + tile rows).
-    // Workgroup rows [0, hot_rows) render the hot tiles hot[0 .. hot_n) of every frame first -- the
+    // Workgroup rows [0, hot_rows) render the hot slots hot[0 .. hot_n) of every frame first -- the
     // tiles the context measured slowest on an earlier frame (rrte_hip.hip, TileProfile) -- and the
     // image-order workgroup of a hot tile exits (its row has a bit in hot_row_bits).  Pixels are
     // independent (raytracer.rs:57-60), so any order renders the same bytes; this one starts the
@@ -120,9 +123,9 @@ struct KParams {
     float* xterms;
     uint32_t* xcount;
     uint32_t light_part[kMaxSplitLights / 16];  // 2 bits per light: the part that shades it
+    const uint32_t* hot;     // device hot list (kHotListWords words; immutable while launches use it)
     uint32_t tiles_x, hot_rows, hot_n;
     uint32_t hot_row_bits[kHotRowWords];
-    uint32_t hot[kMaxHotTiles];
     FrameCam cam[kMaxLaunchFrames];
 };
 static_assert(sizeof(KParams) <= 3584, "kernel arguments stay below the 4 KB kernarg limit");

@@ -2025,11 +2025,12 @@ __device__ __forceinline__ LaunchTile launch_tile(const KParams& kp) {
     }
     t.y = r - kp.hot_rows;
     if ((kp.hot_row_bits[(t.y >> 5) & (kHotRowWords - 1u)] >> (t.y & 31u)) & 1u) {
-        // a row with hot tiles: is this one of them?  lane j tests hot[j], hot[j + 64], ...
+        // a row with hot tiles: is this one of them?  lane j tests the row's slot o0 + j, o0 + j + 64, ...
         const uint32_t me = (t.y << 12) | t.x, lane = threadIdx.x & 63u;
+        const uint32_t o0 = kp.hot[kMaxHotTiles + t.y], o1 = kp.hot[kMaxHotTiles + t.y + 1u];
         bool dup = false;
-        for (uint32_t i = 0; i < kp.hot_n; i += 64u)
-            if (i + lane < kp.hot_n && (kp.hot[i + lane] >> 4) == me) dup = true;
+        for (uint32_t i = o0; i < o1; i += 64u)
+            if (i + lane < o1 && (kp.hot[i + lane] >> 4) == me) dup = true;
         t.run = __ballot(dup) == 0ull;
     }
     return t;

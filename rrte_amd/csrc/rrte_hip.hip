@@ -36,7 +36,7 @@ using namespace rrte;
 
 // Everything one launch of the ray kernel needs, decided on the host from the scene and parameters.
 // A multi-frame launch (batched gather) is one plan whose KParams carry up to kMaxLaunchFrames
-// cameras: blockIdx.z picks the frame.
+// cameras: blockIdx.y picks the frame (KParams::hot: grid (tile columns, frames, hot rows + tile rows)).
 struct LaunchPlan {
     KParams k;
     int mode;
@@ -85,7 +85,7 @@ struct rrte_ctx {
     hipEvent_t last_gather_ev = nullptr;
     // Batched gather (rrte_hip_set_gather_batch, B > 1): a frame call only plans its render (camera,
     // tile rectangles); every B frames (or at rrte_hip_flush / synchronize / a scene or parameter
-    // change) the batch renders in multi-frame launches (blockIdx.z = frame, up to kMaxLaunchFrames
+    // change) the batch renders in multi-frame launches (blockIdx.y = frame, up to kMaxLaunchFrames
     // per launch) on the slab's render stream into the send slab, and the comm stream gathers all B
     // frames to the root in ONE ncclGather and de-interleaves them.  Every collective is issued on
     // the one comm stream, in program order; slab k's render stream overlaps slab k-1's gather.
@@ -190,12 +190,21 @@ struct rrte_ctx {
         uint32_t* h_cost = nullptr; size_t cap_h = 0;  // pinned
         uint32_t tiles = 0, tiles_x = 0;                 // of the pending profile
         // the measured slowest tiles, slowest first (tile index, 100 MHz ticks), and the slot list
-        // composed from them for `slots_parts` parts per split tile
+        // composed from them for `slots_parts` parts per split tile (at most kMaxHotTiles slots)
         std::vector<std::pair<uint32_t, uint32_t>> top;
         uint32_t top_max = 0;
         bool fixed = false;              // RRTE_TILE_ORDER=2 list
         std::vector<uint32_t> slots;     // packed hot_pack slots, ascending
         uint32_t slots_parts = 0;
+        // device copies of slot lists (KParams::hot): a ring of immutable versions, each rewritten only
+        // after the launches that used it have completed
+        static constexpr int kVersions = 4;
+        uint32_t* d_list[kVersions] = {};
+        hipEvent_t ev_list[kVersions] = {};
+        bool list_used[kVersions] = {};
+        uint32_t* h_list = nullptr;      // pinned staging
+        int cur = -1;                    // version holding `slots` (-1: not uploaded)
+        int next_version = 0;
         uint32_t row_bits[kHotRowWords] = {};
         uint64_t launches = 0;           // launches of `key` since its last profile
         uint64_t profiles = 0;           // completed profiles
@@ -1036,6 +1045,7 @@ void compose_slots(rrte_ctx::TileProfile& tp, uint32_t parts, uint32_t tiles_x, 
     tp.slots.clear();
     memset(tp.row_bits, 0, sizeof tp.row_bits);
     tp.slots_parts = parts;
+    tp.cur = -1;
     auto add = [&](uint32_t i, uint32_t np) {
         const uint32_t x = i % tiles_x, y = i / tiles_x;
         for (uint32_t q = 0; q < np; ++q) tp.slots.push_back(hot_pack(x, y, q, np));
@@ -1071,6 +1081,33 @@ uint32_t split_parts(const rrte_ctx* c, const LaunchPlan& L, uint32_t light_part
     for (uint32_t i = 0, q = 0; i < L.num_lights; ++i)
         if (c->h_lights[i].kind != RRTE_LIGHT_AMBIENT) light_part[i >> 4] |= ((q++ % parts) & 3u) << ((i & 15u) * 2u);
     return parts;
+}
+
+// Uploads the composed slots and their tile-row offsets into the next version of the device list
+// (kHotListWords words); false leaves the launch in image order.  The copy completes before any later
+// launch is enqueued (the context's own stream, synchronised), so every launch sees a whole list.
+bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
+    auto& tp = c->tprof;
+    const int pick = tp.next_version;  // the least recently uploaded version
+    tp.next_version = (tp.next_version + 1) % rrte_ctx::TileProfile::kVersions;
+    const size_t bytes = kHotListWords * sizeof(uint32_t);
+    if (!tp.d_list[pick] && hipMalloc(reinterpret_cast<void**>(&tp.d_list[pick]), bytes) != hipSuccess) return false;
+    if (!tp.ev_list[pick] && hipEventCreateWithFlags(&tp.ev_list[pick], hipEventDisableTiming) != hipSuccess) return false;
+    if (!tp.h_list && hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), bytes, hipHostMallocDefault) != hipSuccess) return false;
+    if (tp.list_used[pick] && hipEventSynchronize(tp.ev_list[pick]) != hipSuccess) return false;  // its launches are done
+    memset(tp.h_list, 0, bytes);
+    memcpy(tp.h_list, tp.slots.data(), tp.slots.size() * sizeof(uint32_t));
+    uint32_t* off = tp.h_list + kMaxHotTiles;
+    for (uint32_t y = 0, i = 0; y <= std::min<uint32_t>(tiles_y, kHotRows); ++y) {
+        while (i < tp.slots.size() && hot_y(tp.slots[i]) < y) ++i;
+        off[y] = i;
+    }
+    if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return false;
+    tp.list_used[pick] = false;
+    tp.cur = pick;
+    return true;
 }
 
 // Sets the plan's tile order (hot slots, tile profile) for a launch of kernel `kern`; true when this
@@ -1113,10 +1150,10 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     ++tp.launches;
     const uint32_t parts = split_parts(c, L, k.light_part);
     if ((!tp.top.empty() || tp.fixed) && (tp.slots_parts != parts || tp.slots.empty())) compose_slots(tp, parts, L.gx, tiles);
-    if (!tp.slots.empty()) {
+    if (!tp.slots.empty() && (tp.cur >= 0 || upload_hot_list(c, L.gy))) {
+        k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
         k.hot_rows = (k.hot_n + L.gx - 1) / L.gx;
-        memcpy(k.hot, tp.slots.data(), k.hot_n * sizeof(uint32_t));
         memcpy(k.hot_row_bits, tp.row_bits, sizeof tp.row_bits);
     }
     if (!profile) return false;
@@ -1143,7 +1180,7 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
     area = -1;
     KParams& k = L.k;
     bool any = false;
-    for (uint32_t i = 0; i < k.hot_n && !any; ++i) any = hot_parts(k.hot[i]) > 1;
+    for (uint32_t i = 0; i < k.hot_n && !any; ++i) any = hot_parts(c->tprof.slots[i]) > 1;
     if (!any) return RRTE_OK;
     area = c->xnext;
     c->xnext = (c->xnext + 1) % rrte_ctx::kXAreas;
@@ -1179,13 +1216,17 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
 
 // Queues the profiled launch's copy-back on its stream (plan_tile_order returned true) and marks the
 // launch's split exchange area busy until the launch completes.
-rrte_status finish_tile_order(rrte_ctx* c, bool profile, int area, hipStream_t st) {
+rrte_status finish_tile_order(rrte_ctx* c, const LaunchPlan& L, bool profile, int area, hipStream_t st) {
+    auto& tp = c->tprof;
+    if (L.k.hot_n && tp.cur >= 0 && L.k.hot == tp.d_list[tp.cur]) {
+        HIPCHK(c, hipEventRecord(tp.ev_list[tp.cur], st));
+        tp.list_used[tp.cur] = true;
+    }
     if (area >= 0) {
         HIPCHK(c, hipEventRecord(c->xarea[area].ev, st));
         c->xarea[area].used = true;
     }
     if (!profile) return RRTE_OK;
-    auto& tp = c->tprof;
     HIPCHK(c, hipMemcpyAsync(tp.h_cost, tp.d_cost, (size_t)tp.tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipEventRecord(tp.ev, st));
     tp.pending = true;
@@ -1216,7 +1257,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         else
             HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, st, args, nullptr));
         hs.lap(8);
-        return finish_tile_order(c, profile, area, st);
+        return finish_tile_order(c, L, profile, area, st);
     }
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
                  c->mesh_view};
@@ -1228,7 +1269,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     else
         hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     HIPCHK(c, hipGetLastError());
-    return finish_tile_order(c, profile, area, st);
+    return finish_tile_order(c, L, profile, area, st);
 }
 
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
@@ -1414,6 +1455,11 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->tprof.d_cost) (void)hipFree(c->tprof.d_cost);
     if (c->tprof.h_cost) (void)hipHostFree(c->tprof.h_cost);
     if (c->tprof.ev) (void)hipEventDestroy(c->tprof.ev);
+    for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i) {
+        if (c->tprof.d_list[i]) (void)hipFree(c->tprof.d_list[i]);
+        if (c->tprof.ev_list[i]) (void)hipEventDestroy(c->tprof.ev_list[i]);
+    }
+    if (c->tprof.h_list) (void)hipHostFree(c->tprof.h_list);
     for (auto& xa : c->xarea) {
         if (xa.terms) (void)hipFree(xa.terms);
         if (xa.count) (void)hipFree(xa.count);

@@ -49,10 +49,13 @@ def _render(ctx, sc, prm, rows=None):
     return (rgba.cpu().numpy().view(np.uint8), f32.cpu().numpy().view(np.uint32), s1.shadow_rays, s1.hot_tiles)
 
 
+MAX_SLOTS = 1024  # device_scene.hpp kMaxHotTiles
+
+
 def _fixed_slots(tiles, parts):
     """Slots of RRTE_TILE_ORDER=2's list (rrte_hip.hip compose_slots): m tiles, every other one split."""
-    m = min(tiles, 256)
-    while m > 1 and (m + 1) // 2 * parts + m // 2 > 256:
+    m = min(tiles, MAX_SLOTS)
+    while m > 1 and (m + 1) // 2 * parts + m // 2 > MAX_SLOTS:
         m -= 1
     return (m + 1) // 2 * parts + m // 2
 
@@ -117,7 +120,7 @@ def test_fixed_hot_list_at_4k(monkeypatch):
     ref = _ctx(monkeypatch, "0", abi.JIT_ON)
     hot = _ctx(monkeypatch, "2", abi.JIT_ON)
     a, b = _render(ref, sc, prm), _render(hot, sc, prm)
-    assert b[3] == 256  # 3 lights: 64 split tiles of 3 parts + 64 whole ones
+    assert b[3] == _fixed_slots(480 * 270, 3)  # 3 lights: 256 split tiles of 3 parts + 256 whole ones
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
     ref.close()
     hot.close()
@@ -139,7 +142,7 @@ def test_measured_hot_list(monkeypatch):
         got = _render(ctx, sc, prm)
         assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[2]
         seen = max(seen, got[3])
-    assert 0 < seen <= 256
+    assert 0 < seen <= MAX_SLOTS
     ctx.close()
 
 
@@ -173,7 +176,7 @@ def test_fixed_hot_list_in_batched_gathers(monkeypatch):
                                                     C.c_void_p(streams[i % 2].cuda_stream)))
     ctx.check(lib.rrte_hip_flush(ctx.h))
     ctx.check(lib.rrte_hip_synchronize(ctx.h))
-    assert ctx.stats().hot_tiles == 256  # per launch: 64 split tiles x 3 parts + 64 whole tiles
+    assert ctx.stats().hot_tiles == _fixed_slots(40 * 25, 3)  # per launch: split tiles x 3 parts + whole tiles
     for i, o in enumerate(outs):
         got = o.cpu().numpy().view(np.uint8)
         assert np.array_equal(got, want[i]), f"frame {i}: {(got != want[i]).sum()} bytes differ"

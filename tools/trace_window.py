@@ -15,8 +15,11 @@ for r in rows:
     r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
 rows.sort(key=lambda r: r["s"])
 ray = [r for r in rows if "rrte_jit_kernel" in r["Kernel_Name"] or "ray_kernel" in r["Kernel_Name"]]
-if any(int(r.get("Grid_Size_Z") or 1) > 1 for r in ray):
-    ray = [r for r in ray if int(r.get("Grid_Size_Z") or 1) > 1]  # batched path: the multi-frame launches only
+# multi-frame launches: grid (tile columns, frames, hot rows + tile rows) -- frames in y since the hot-first
+# tile order (round 3); in z before it
+FR = "Grid_Size_Y"
+if any(int(r.get(FR) or 1) > 1 for r in ray):
+    ray = [r for r in ray if int(r.get(FR) or 1) > 1]  # batched path: the multi-frame launches only
 w0 = ray[-n]["s"]
 # the window: from the first of those launches to the end of the last kernel that follows the last one
 # before the next launch of another kind of frame (the bench's later single-frame measurements)
