@@ -1914,6 +1914,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
         // every term store performed (vmcnt 0) before this part counts itself in; the last part's
         // loads are issued after its count returns (a uniform branch on it)
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (kp.flags & kFlagSplitFence) __threadfence();
         __builtin_amdgcn_s_waitcnt(0);
         uint32_t old = 0u;
         if (lane == 0u) old = __hip_atomic_fetch_add(sp.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1923,6 +1924,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             sp.skip_store = true;
             return out;
         }
+        if (kp.flags & kFlagSplitFence) __threadfence();
         if (lane == 0u) __hip_atomic_store(sp.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next use
         if (hit) {
             for (uint32_t li = 0; li < kp.num_lights; ++li) {

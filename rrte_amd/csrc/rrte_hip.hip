@@ -45,6 +45,8 @@ struct LaunchPlan {
     uint32_t gx, gy;
 };
 
+constexpr double kSplitFracDefault = 0.7;  // see compose_slots
+
 struct rrte_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -221,6 +223,8 @@ struct rrte_ctx {
     XArea xarea[kXAreas];
     int xnext = 0;
     bool env_tile_split = true;        // RRTE_TILE_SPLIT=0: hot tiles are never split (A/B)
+    double split_frac = kSplitFracDefault;  // RRTE_SPLIT_FRAC
+    bool env_split_fence = false;      // RRTE_SPLIT_FENCE=1 (diagnostics): agent-scope fences around split counts
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
@@ -1036,12 +1040,12 @@ void build_hot_list(rrte_ctx::TileProfile& tp) {
     tp.top_max = mx;
 }
 
-// Split tiles: a hot tile at least this fraction of the slowest one is rendered as one part per
-// shadow-casting light (at most 4), so its lights' shadow marches run on different waves at once.
-constexpr double kSplitFrac = 0.5;
+// Split tiles: a hot tile at least this fraction of the slowest one (RRTE_SPLIT_FRAC, default 0.7) is
+// rendered as one part per shadow-casting light (at most 4), so its lights' shadow marches run on
+// different waves at once; every part repeats the tile's camera rays, so only the tail tiles pay.
 
 // Hot slots for `parts` parts per split tile (1: no splitting), ascending.
-void compose_slots(rrte_ctx::TileProfile& tp, uint32_t parts, uint32_t tiles_x, uint32_t tiles) {
+void compose_slots(rrte_ctx::TileProfile& tp, uint32_t parts, uint32_t tiles_x, uint32_t tiles, double split_frac) {
     tp.slots.clear();
     memset(tp.row_bits, 0, sizeof tp.row_bits);
     tp.slots_parts = parts;
@@ -1059,7 +1063,7 @@ void compose_slots(rrte_ctx::TileProfile& tp, uint32_t parts, uint32_t tiles_x, 
         for (uint32_t j = 0; j < m; ++j) add(m > 1 ? (uint32_t)((uint64_t)j * (tiles - 1) / (m - 1)) : 0u, j % 2 ? 1u : parts);
     } else {
         for (const auto& t : tp.top) {
-            const uint32_t np = parts > 1 && t.second >= kSplitFrac * tp.top_max ? parts : 1u;
+            const uint32_t np = parts > 1 && t.second >= split_frac * tp.top_max ? parts : 1u;
             if (tp.slots.size() + np > kMaxHotTiles) break;
             add(t.first, np);
         }
@@ -1149,7 +1153,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     const bool profile = !tp.pending && tp.launches >= kTileReprofile;
     ++tp.launches;
     const uint32_t parts = split_parts(c, L, k.light_part);
-    if ((!tp.top.empty() || tp.fixed) && (tp.slots_parts != parts || tp.slots.empty())) compose_slots(tp, parts, L.gx, tiles);
+    if ((!tp.top.empty() || tp.fixed) && (tp.slots_parts != parts || tp.slots.empty())) compose_slots(tp, parts, L.gx, tiles, c->split_frac);
     if (!tp.slots.empty() && (tp.cur >= 0 || upload_hot_list(c, L.gy))) {
         k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
@@ -1211,6 +1215,7 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
     if (xa.used && hipEventQuery(xa.ev) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(st, xa.ev, 0));
     k.xterms = xa.terms;
     k.xcount = xa.count;
+    if (c->env_split_fence) k.flags |= kFlagSplitFence;
     return RRTE_OK;
 }
 
@@ -1396,6 +1401,8 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         c->env_tile_order_fixed = g[0] == '2';
     }
     if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] != '0';
+    if (const char* g = getenv("RRTE_SPLIT_FRAC"); g && *g) c->split_frac = strtod(g, nullptr);
+    if (const char* g = getenv("RRTE_SPLIT_FENCE")) c->env_split_fence = g[0] == '1';
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
