@@ -135,9 +135,7 @@ static_assert(sizeof(KParams) <= 3584, "kernel arguments stay below the 4 KB ker
 // only when it has proved every pixel's alpha byte is 255 (rrte_hip.hip, slab_rgb24), and the
 // root's de-interleave puts the 255 back.
 constexpr uint32_t kFlagSlabRgb24 = 1u << 31;
-// Internal flag (diagnostics, RRTE_SPLIT_FENCE=1): split tiles also fence at agent scope around their
-// arrival count (L2 write-back / invalidate), on top of the uncached exchange.
-constexpr uint32_t kFlagSplitFence = 1u << 30;
+
 
 // ---------------------------------------------------------------- f32 vec3
 struct f3 { float x, y, z; };

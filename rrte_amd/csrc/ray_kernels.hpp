@@ -1816,12 +1816,10 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
     // RRTE_DEBUG bit 8 (timing diagnostics only, wrong images): shadow tests for light (debug >> 9) & 7 only
     const bool split = sp.parts > 1u;
     const uint32_t lane = threadIdx.x & 63u;
-    // exchange through uncached memory (hipDeviceMallocUncached) with agent-scope atomic stores and
-    // loads: coherent across the XCDs' L2s without the agent-scope fences' L2 write-back/invalidate
     auto publish = [&](uint32_t li, float tr, float tg, float tb) {
-        __hip_atomic_store(sp.terms + (li * 3u + 0u) * 64u + lane, tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sp.terms + (li * 3u + 1u) * 64u + lane, tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sp.terms + (li * 3u + 2u) * 64u + lane, tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sp.terms[(li * 3u + 0u) * 64u + lane] = tr;
+        sp.terms[(li * 3u + 1u) * 64u + lane] = tg;
+        sp.terms[(li * 3u + 2u) * 64u + lane] = tb;
     };
     auto shade = [&](const DLight& l, uint64_t smask, uint32_t li) {
         if (split && light_part(kp, li) != sp.part) return;  // another part's light
@@ -1911,26 +1909,24 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
         }
     }
     if (split) {
-        // every term store performed (vmcnt 0) before this part counts itself in; the last part's
-        // loads are issued after its count returns (a uniform branch on it)
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (kp.flags & kFlagSplitFence) __threadfence();
-        __builtin_amdgcn_s_waitcnt(0);
+        // publish (agent-scope release fence), count in; the last part to arrive acquires and sums in
+        // light order.  (An exchange through uncached memory with atomic stores and loads and no
+        // fences was faster and failed one 4K parity run in three: not kept.)
+        __threadfence();
         uint32_t old = 0u;
-        if (lane == 0u) old = __hip_atomic_fetch_add(sp.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0u) old = atomicAdd(sp.count, 1u);
         old = (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (old + 1u != sp.parts) {
             sp.skip_store = true;
             return out;
         }
-        if (kp.flags & kFlagSplitFence) __threadfence();
+        __threadfence();
         if (lane == 0u) __hip_atomic_store(sp.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next use
         if (hit) {
             for (uint32_t li = 0; li < kp.num_lights; ++li) {
-                cr = cr + __hip_atomic_load(sp.terms + (li * 3u + 0u) * 64u + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                cg = cg + __hip_atomic_load(sp.terms + (li * 3u + 1u) * 64u + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                cb = cb + __hip_atomic_load(sp.terms + (li * 3u + 2u) * 64u + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                cr = cr + sp.terms[(li * 3u + 0u) * 64u + lane];
+                cg = cg + sp.terms[(li * 3u + 1u) * 64u + lane];
+                cb = cb + sp.terms[(li * 3u + 2u) * 64u + lane];
             }
         }
     }

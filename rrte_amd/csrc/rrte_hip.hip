@@ -198,12 +198,12 @@ struct rrte_ctx {
         bool fixed = false;              // RRTE_TILE_ORDER=2 list
         std::vector<uint32_t> slots;     // packed hot_pack slots, ascending
         uint32_t slots_parts = 0;
-        // device copies of slot lists (KParams::hot): a ring of immutable versions, each rewritten only
-        // after the launches that used it have completed
-        static constexpr int kVersions = 4;
+        // device copies of slot lists (KParams::hot): a pool of immutable versions, one per upload; when
+        // the pool is used up the device is synchronised once and every version is free again (no
+        // per-launch bookkeeping: an event recorded after each launch put a gap between the launches
+        // of one stream)
+        static constexpr int kVersions = 16;
         uint32_t* d_list[kVersions] = {};
-        hipEvent_t ev_list[kVersions] = {};
-        bool list_used[kVersions] = {};
         uint32_t* h_list = nullptr;      // pinned staging
         int cur = -1;                    // version holding `slots` (-1: not uploaded)
         int next_version = 0;
@@ -222,9 +222,8 @@ struct rrte_ctx {
     static constexpr int kXAreas = 8;
     XArea xarea[kXAreas];
     int xnext = 0;
-    bool env_tile_split = true;        // RRTE_TILE_SPLIT=0: hot tiles are never split (A/B)
+    bool env_tile_split = false;       // RRTE_TILE_SPLIT=1: split the slowest hot tiles (measured slower)
     double split_frac = kSplitFracDefault;  // RRTE_SPLIT_FRAC
-    bool env_split_fence = false;      // RRTE_SPLIT_FENCE=1 (diagnostics): agent-scope fences around split counts
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
@@ -1092,13 +1091,16 @@ uint32_t split_parts(const rrte_ctx* c, const LaunchPlan& L, uint32_t light_part
 // launch is enqueued (the context's own stream, synchronised), so every launch sees a whole list.
 bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
     auto& tp = c->tprof;
-    const int pick = tp.next_version;  // the least recently uploaded version
-    tp.next_version = (tp.next_version + 1) % rrte_ctx::TileProfile::kVersions;
+    if (tp.next_version == rrte_ctx::TileProfile::kVersions) {
+        // every version may still be read by a launch in flight: wait for all of them, once per
+        // kVersions uploads (one upload per profile, i.e. per kTileReprofile launches at most)
+        if (hipDeviceSynchronize() != hipSuccess) return false;
+        tp.next_version = 0;
+    }
+    const int pick = tp.next_version++;
     const size_t bytes = kHotListWords * sizeof(uint32_t);
     if (!tp.d_list[pick] && hipMalloc(reinterpret_cast<void**>(&tp.d_list[pick]), bytes) != hipSuccess) return false;
-    if (!tp.ev_list[pick] && hipEventCreateWithFlags(&tp.ev_list[pick], hipEventDisableTiming) != hipSuccess) return false;
     if (!tp.h_list && hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), bytes, hipHostMallocDefault) != hipSuccess) return false;
-    if (tp.list_used[pick] && hipEventSynchronize(tp.ev_list[pick]) != hipSuccess) return false;  // its launches are done
     memset(tp.h_list, 0, bytes);
     memcpy(tp.h_list, tp.slots.data(), tp.slots.size() * sizeof(uint32_t));
     uint32_t* off = tp.h_list + kMaxHotTiles;
@@ -1109,7 +1111,6 @@ bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
     if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return false;
-    tp.list_used[pick] = false;
     tp.cur = pick;
     return true;
 }
@@ -1192,7 +1193,7 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
     const size_t groups = (size_t)k.hot_n * k.nframes;
     const size_t terms = groups * k.num_lights * 3u * 64u;
     if (xa.cap_terms < terms || xa.cap_count < groups) {
-        // every area of the ring at once, uncached (the kernel's exchange relies on it), sized for the
+        // every area of the ring at once, sized for the
         // largest launch (kMaxHotTiles slots x kMaxLaunchFrames frames) of this light count: one device
         // synchronisation at the first split launch, none later
         HIPCHK(c, hipDeviceSynchronize());
@@ -1203,8 +1204,8 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
             a.terms = nullptr;
             a.count = nullptr;
             a.cap_terms = a.cap_count = 0;
-            HIPCHK(c, hipExtMallocWithFlags(reinterpret_cast<void**>(&a.terms), tmax * sizeof(float), hipDeviceMallocUncached));
-            HIPCHK(c, hipExtMallocWithFlags(reinterpret_cast<void**>(&a.count), gmax * sizeof(uint32_t), hipDeviceMallocUncached));
+            HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&a.terms), tmax * sizeof(float)));
+            HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&a.count), gmax * sizeof(uint32_t)));
             HIPCHK(c, hipMemset(a.count, 0, gmax * sizeof(uint32_t)));
             a.cap_terms = tmax;
             a.cap_count = gmax;
@@ -1215,7 +1216,6 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
     if (xa.used && hipEventQuery(xa.ev) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(st, xa.ev, 0));
     k.xterms = xa.terms;
     k.xcount = xa.count;
-    if (c->env_split_fence) k.flags |= kFlagSplitFence;
     return RRTE_OK;
 }
 
@@ -1223,10 +1223,7 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
 // launch's split exchange area busy until the launch completes.
 rrte_status finish_tile_order(rrte_ctx* c, const LaunchPlan& L, bool profile, int area, hipStream_t st) {
     auto& tp = c->tprof;
-    if (L.k.hot_n && tp.cur >= 0 && L.k.hot == tp.d_list[tp.cur]) {
-        HIPCHK(c, hipEventRecord(tp.ev_list[tp.cur], st));
-        tp.list_used[tp.cur] = true;
-    }
+    (void)L;
     if (area >= 0) {
         HIPCHK(c, hipEventRecord(c->xarea[area].ev, st));
         c->xarea[area].used = true;
@@ -1400,9 +1397,8 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         c->env_tile_order = g[0] != '0';
         c->env_tile_order_fixed = g[0] == '2';
     }
-    if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] != '0';
+    if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] == '1';
     if (const char* g = getenv("RRTE_SPLIT_FRAC"); g && *g) c->split_frac = strtod(g, nullptr);
-    if (const char* g = getenv("RRTE_SPLIT_FENCE")) c->env_split_fence = g[0] == '1';
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
@@ -1464,7 +1460,6 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->tprof.ev) (void)hipEventDestroy(c->tprof.ev);
     for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i) {
         if (c->tprof.d_list[i]) (void)hipFree(c->tprof.d_list[i]);
-        if (c->tprof.ev_list[i]) (void)hipEventDestroy(c->tprof.ev_list[i]);
     }
     if (c->tprof.h_list) (void)hipHostFree(c->tprof.h_list);
     for (auto& xa : c->xarea) {

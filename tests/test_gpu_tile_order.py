@@ -4,10 +4,10 @@ one workgroup per shadow-casting light, the last of which sums the lights' terms
 Pixels are independent (raytracer.rs:57-60) and adding a light that contributes nothing as +0 is
 exact, so every order and split must give the same bytes, linear floats and shadow-ray counts as
 image order.  RRTE_TILE_ORDER=2 forces a fixed list of tiles spread over the frame (first and last
-tile included, every other one split where splitting applies) on every launch, so these tests run
-the hot slots, split parts, the partial hot row and the image-order skip on every kernel kind, mode
-and launch shape; RRTE_TILE_ORDER=0 is image order, RRTE_TILE_SPLIT=0 hot order without splits; the
-default measures the tiles on a profiled launch and uses the measured list once its copy arrives."""
+tile included, every other one split when RRTE_TILE_SPLIT=1 and splitting applies) on every launch,
+so these tests run the hot slots, split parts, the partial hot row and the image-order skip on every
+kernel kind, mode and launch shape; RRTE_TILE_ORDER=0 is image order.  The default measures the tiles
+on a profiled launch and uses the measured list (no splits: measured slower) once its copy arrives."""
 import ctypes as C
 
 import numpy as np
@@ -118,7 +118,7 @@ def test_fixed_hot_list_at_4k(monkeypatch):
     objs, lights, cam, cfg = scenes.sdf_showcase(3840, 2160)
     sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
     ref = _ctx(monkeypatch, "0", abi.JIT_ON)
-    hot = _ctx(monkeypatch, "2", abi.JIT_ON)
+    hot = _ctx(monkeypatch, "2", abi.JIT_ON, RRTE_TILE_SPLIT="1")
     a, b = _render(ref, sc, prm), _render(hot, sc, prm)
     assert b[3] == _fixed_slots(480 * 270, 3)  # 3 lights: 256 split tiles of 3 parts + 256 whole ones
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
@@ -163,7 +163,7 @@ def test_fixed_hot_list_in_batched_gathers(monkeypatch):
         ref.check(ref.lib.rrte_hip_render(ref.h, sc.ref(), C.byref(prm), buf.ctypes.data_as(C.POINTER(C.c_uint8))))
         want.append(buf)
     ref.close()
-    ctx = _ctx(monkeypatch, "2", abi.JIT_ON, RRTE_FORCE_GATHER="1")
+    ctx = _ctx(monkeypatch, "2", abi.JIT_ON, RRTE_FORCE_GATHER="1", RRTE_TILE_SPLIT="1")
     lib = ctx.lib
     uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
     ctx.check(lib.rrte_hip_comm_unique_id(uid))
