@@ -69,6 +69,7 @@ def test_4k_rank_shares_match_oracle_rows(nranks, oracle_4k, monkeypatch):
         img_rows = [y for y in range(H) if (y // BAND) % nranks == rank]
         assert len(img_rows) == rows
         f32 = torch.zeros(rows * W * 4, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
         ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), None, f32.data_ptr(), None))
         ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
         st = ctx.stats()

@@ -29,6 +29,7 @@ def test_blocking_render_matches_device_path(name, w, h):
     prm = cfg.lower()
     ctx = Context(0, jit=abi.JIT_ON)
     dev = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), dev.data_ptr(), None, None))
     ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
     want = dev.cpu().numpy().view(np.uint8)

@@ -66,9 +66,11 @@ def test_local_calls_render_but_do_not_close_a_batch(monkeypatch):
     _comm(ctx)
     ctx.check(ctx.lib.rrte_hip_set_gather_batch(ctx.h, 4))
     outs = [torch.full((W * H,), -1, dtype=torch.int32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     for (sc, prm), o in zip(frames[:3], outs):
         ctx.check(_gather(ctx, sc, prm, o))
     pv = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, preview[0].ref(), C.byref(preview[1]), pv.data_ptr(), None, None))
     ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
     assert np.array_equal(pv.cpu().numpy().view(np.uint8), want[4])
@@ -92,6 +94,7 @@ def test_comm_init_gathers_the_open_batch_first(monkeypatch):
     _comm(ctx)
     ctx.check(ctx.lib.rrte_hip_set_gather_batch(ctx.h, 4))
     outs = [torch.full((W * H,), -1, dtype=torch.int32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     for (sc, prm), o in zip(frames[:2], outs):
         ctx.check(_gather(ctx, sc, prm, o))
     _comm(ctx)
@@ -121,6 +124,7 @@ def test_stalled_gather_surfaces_as_error(batch, monkeypatch):
     ctx.check(ctx.lib.rrte_hip_set_gather_batch(ctx.h, batch))
     stream = torch.cuda.Stream()
     outs = [torch.full((W * H,), -1, dtype=torch.int32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     for (sc, prm), o in zip(frames[:2 * batch], outs):  # collectives 1 and 2 (the stalled one)
         ctx.check(_gather(ctx, sc, prm, o, stream))
     t0 = time.perf_counter()

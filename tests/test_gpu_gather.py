@@ -77,6 +77,7 @@ def _check_gather(overlap, jit, batch, monkeypatch, alpha):
     dev = torch.device("cuda", 0)
     streams = [torch.cuda.Stream(dev) for _ in range(3)]  # frames in flight, as bench.py runs them
     outs = [torch.empty(w * h, dtype=torch.int32, device=dev) for _ in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
         p = abi.RenderParams.from_buffer_copy(prm)
         if overlap:
@@ -138,6 +139,7 @@ def test_gather_batch_arguments_and_size_change(monkeypatch):
     ref.close()
     streams = [torch.cuda.Stream() for _ in range(2)]
     outs = [torch.empty(p.width * p.height, dtype=torch.int32, device="cuda") for _, p in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
         ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
                                                     C.c_void_p(streams[i % 2].cuda_stream)))
@@ -177,6 +179,7 @@ def test_gather_batch_multi_frame_launches_and_changes(monkeypatch):
         ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 16))
         streams = [torch.cuda.Stream() for _ in range(2)]
         outs = [torch.full((p.width * p.height,), -1, dtype=torch.int32, device="cuda") for _, p in frames]
+        torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
         for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
             ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
                                                         C.c_void_p(streams[i % 2].cuda_stream)))
@@ -215,6 +218,7 @@ def test_query_reports_batched_work_done(monkeypatch):
     ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 4))
     stream = torch.cuda.Stream()
     outs = [torch.full((p.width * p.height,), -1, dtype=torch.int32, device="cuda") for _, p in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     torch.cuda.synchronize()
     for (sc, prm), o in zip(frames, outs):
         ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),

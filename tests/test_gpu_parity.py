@@ -326,6 +326,7 @@ def test_camera_tile_culling_with_band_mapping(band, jit, monkeypatch):
             out = {}
             for tc, ctx in ctxs.items():
                 f32 = torch.zeros(rows * w * 4, dtype=torch.float32, device="cuda")
+                torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
                 ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), None, f32.data_ptr(), None))
                 ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
                 out[tc] = f32.cpu().numpy().view(np.uint32).reshape(rows, w, 4)
@@ -361,6 +362,7 @@ def test_jit_cache_eviction_with_frames_in_flight(monkeypatch):
         sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
         for j in range(3):  # several frames of each variant in flight on different streams
             buf = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
             st = streams[(i + j) % 4]
             ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), buf.data_ptr(), None,
                                                     C.c_void_p(st.cuda_stream)))
@@ -398,6 +400,7 @@ def test_async_device_output_matches_blocking():
     sc = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
     buf = torch.zeros(320 * 180, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     s = torch.cuda.Stream()
     ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), buf.data_ptr(), None,
                                             C.c_void_p(s.cuda_stream)))

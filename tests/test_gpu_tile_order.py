@@ -39,11 +39,13 @@ def _render(ctx, sc, prm, rows=None):
     rows = prm.height if rows is None else rows
     p = abi.RenderParams.from_buffer_copy(prm)
     rgba = torch.full((rows * p.width,), -1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(p), rgba.data_ptr(), None, None))
     ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
     s1 = ctx.stats()
     p.flags |= abi.FLAG_F32_LINEAR
     f32 = torch.zeros(rows * p.width * 4, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(p), None, f32.data_ptr(), None))
     ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
     return (rgba.cpu().numpy().view(np.uint8), f32.cpu().numpy().view(np.uint32), s1.shadow_rays, s1.hot_tiles)
@@ -171,6 +173,7 @@ def test_fixed_hot_list_in_batched_gathers(monkeypatch):
     ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, 8))
     streams = [torch.cuda.Stream() for _ in range(2)]
     outs = [torch.full((p.width * p.height,), -1, dtype=torch.int32, device="cuda") for _, p in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
     for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
         ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
                                                     C.c_void_p(streams[i % 2].cuda_stream)))
