@@ -472,6 +472,8 @@ def main():
         line["primary_only"] = {"value": round(primary / elapsed / 1e6, 3), "unit": "Mray/s"}
         line["frame_latency_ms"] = round(latency_ms, 4)
         line["host_enqueue_ms_per_step"] = round((t_enq - t0) / args.steps * 1e3, 4)
+        # hot-first tile order: slots of the timed frames' launches dispatched first
+        line["tile_order"] = {"hot_slots": int(st.hot_tiles), "env": os.environ.get("RRTE_TILE_ORDER", "1")}
         line["d2h_ms"] = round(d2h_ms, 4)  # frame to pinned host memory, excluded from `value`
         if pmc and pmc.get("valu") is not None:
             line["valu"] = dict(pmc["valu"])

@@ -390,10 +390,7 @@ rrte_status rrte_hip_set_comm_timeout(rrte_ctx* ctx, uint32_t ms);
  * scene change through rrte_hip_render / render_f32 / render_async only RENDER the open batch's
  * frames (with the scene they were issued with) and leave its gather for the next collective close,
  * so one rank may poll or render a preview on its own.  frames in [1, 16]; every rank must use the
- * same setting.  Flushing with no open batch does nothing.  After rrte_hip_set_gather_batch,
- * rrte_hip_flush and rrte_hip_comm_init the batches ramp up (2, 4, 8, ... frames, up to `frames`) so the
- * first render starts early; env RRTE_GATHER_RAMP=0 turns the ramp off.  Both are collective, so every
- * rank still closes its batches after the same frames. */
+ * same setting.  Flushing with no open batch does nothing. */
 rrte_status rrte_hip_set_gather_batch(rrte_ctx* ctx, uint32_t frames);
 rrte_status rrte_hip_flush(rrte_ctx* ctx);
 

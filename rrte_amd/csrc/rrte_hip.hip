@@ -112,8 +112,6 @@ struct rrte_ctx {
         hipEvent_t ev_src[kMaxBatch] = {};   // recorded on src[i] at the flush
     } batch;
     int bslot = 0;
-    uint32_t batch_ramp = 2;                 // frames of the next batch while ramping up (gather_frame)
-    bool env_gather_ramp = true;             // RRTE_GATHER_RAMP=0: every batch holds gather_batch frames (A/B)
     bool env_comm_priority = true;           // RRTE_COMM_PRIORITY=0: comm stream at default priority (A/B)
     int batch_slabs = 3;                     // slabs in the ring (RRTE_BATCH_SLABS, A/B: 1..kBatchSlabs; 3 measured
                                              // best against 4 and 6, tools/runs/r03_call16.sh)
@@ -1395,7 +1393,6 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_BATCH_SLABS"); g && *g)
         c->batch_slabs = std::max(1, std::min(rrte_ctx::kBatchSlabs, (int)strtol(g, nullptr, 0)));
     if (const char* g = getenv("RRTE_GATHER_INPLACE")) c->env_gather_inplace = g[0] != '0';
-    if (const char* g = getenv("RRTE_GATHER_RAMP")) c->env_gather_ramp = g[0] != '0';
     if (const char* g = getenv("RRTE_COMM_PRIORITY")) c->env_comm_priority = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
@@ -1691,7 +1688,6 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
     c->comm_failed = false;
     c->comm_fail_msg.clear();
     c->gathers_issued = 0;
-    c->batch_ramp = 2u;
     if (fr != RRTE_OK) return fr;
     ncclUniqueId id;
     memcpy(&id, id_bytes, sizeof id);
@@ -1994,15 +1990,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             if ((r = flush_batch(c)) != RRTE_OK) return r;
         const int k = c->bslot;
         if (b.n == 0) {
-            // ramp (RRTE_GATHER_RAMP, default on): after a reset point the batches hold 2, 4, 8, ...
-            // frames up to the batch size, so the first render starts after two frame calls instead of
-            // a whole batch.  The reset points (rrte_hip_flush, set_gather_batch, comm_init) are
-            // collective calls, so every rank closes its batches after the same frames.
             b.cap = c->gather_batch;
-            if (c->env_gather_ramp) {
-                b.cap = std::min<uint32_t>(c->gather_batch, c->batch_ramp);
-                c->batch_ramp = std::min<uint32_t>(c->batch_ramp * 2u, (uint32_t)rrte_ctx::kMaxBatch);
-            }
             b.width = p->width;
             b.height = p->height;
             b.band = band;
@@ -2103,13 +2091,11 @@ rrte_status rrte_hip_set_gather_batch(rrte_ctx* c, uint32_t frames) {
     rrte_status r = flush_batch(c);
     if (r != RRTE_OK) return r;
     c->gather_batch = frames;
-    c->batch_ramp = 2u;
     return RRTE_OK;
 }
 
 rrte_status rrte_hip_flush(rrte_ctx* c) {
     if (!c) return RRTE_INVALID_ARG;
-    c->batch_ramp = 2u;  // the next batches ramp up again (collective reset point)
     return flush_batch(c);
 }
 

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Evidence only: the ramp was removed after this run -- RRTE_GATHER_RAMP no longer exists.)
 # Emulated N=8 rank-0 batched frame (RRTE_EMULATE_RANK=8:0, RRTE_BENCH_GATHER=1) with the batch ramp
 # (RRTE_GATHER_RAMP) and the high-priority comm stream (RRTE_COMM_PRIORITY) on and off, interleaved
 # rounds at the driver's 20 steps and at 200; then the gather and comm test files.
