@@ -465,6 +465,7 @@ def main():
                 "jit_compile_ms": round(st.jit_compile_ms, 1) if st.jit_active else None,
                 "avg_launch_ms": round(avg_launch_ms, 5),
                 "avg_launch_note": f"HIP events around {len(launch_ms)} frames run one after another on one stream",
+                "launch_ms_each": [round(x, 4) for x in launch_ms],
                 "bytes_per_launch": bytes_per_launch,
                 "note": "VALU-bound path (no dense contraction, no MFMA); HBM traffic is the 4 B/pixel frame store",
             },
