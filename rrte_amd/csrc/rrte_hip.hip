@@ -1013,7 +1013,7 @@ LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_pa
 }
 
 // Hot-first tile order (rrte_ctx::TileProfile, KParams::hot).
-constexpr uint64_t kTileReprofile = 64;  // launches of one shape between two profiles
+constexpr uint64_t kTileReprofile = 256;  // launches of one shape between two profiles (each costs a list upload)
 
 // The slowest tiles of a completed profile: at most kMaxHotTiles, each at least twice the mean tile
 // time and a quarter of the slowest, slowest first.
@@ -1030,13 +1030,20 @@ void build_hot_list(rrte_ctx::TileProfile& tp) {
         sum += tp.h_cost[i];
         mx = std::max(mx, tp.h_cost[i]);
     }
+    // the candidates above the threshold first (a few percent of the tiles), then a sort of those
+    // only: this runs on the host inside a render call (a partial sort over every tile took ~0.7 ms)
     const double thr = std::max(2.0 * sum / n, 0.25 * mx);
-    std::vector<uint32_t> idx(n);
-    for (uint32_t i = 0; i < n; ++i) idx[i] = i;
-    const uint32_t k = std::min<uint32_t>(n, kMaxHotTiles);
-    std::partial_sort(idx.begin(), idx.begin() + k, idx.end(),
-                      [&](uint32_t a, uint32_t b) { return tp.h_cost[a] > tp.h_cost[b] || (tp.h_cost[a] == tp.h_cost[b] && a < b); });
-    for (uint32_t j = 0; j < k && (double)tp.h_cost[idx[j]] >= thr; ++j) tp.top.emplace_back(idx[j], tp.h_cost[idx[j]]);
+    const uint32_t t = (uint32_t)std::min<double>(std::ceil(thr), 4294967295.0);
+    for (uint32_t i = 0; i < n; ++i)
+        if (tp.h_cost[i] >= t) tp.top.emplace_back(i, tp.h_cost[i]);
+    auto slower = [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
+        return a.second > b.second || (a.second == b.second && a.first < b.first);
+    };
+    if (tp.top.size() > kMaxHotTiles) {
+        std::nth_element(tp.top.begin(), tp.top.begin() + kMaxHotTiles, tp.top.end(), slower);
+        tp.top.resize(kMaxHotTiles);
+    }
+    std::sort(tp.top.begin(), tp.top.end(), slower);
     tp.top_max = mx;
 }
 
