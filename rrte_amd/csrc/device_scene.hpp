@@ -125,9 +125,6 @@ struct KParams {
     uint32_t light_part[kMaxSplitLights / 16];  // 2 bits per light: the part that shades it
     const uint32_t* hot;     // device hot list (kHotListWords words; immutable while launches use it)
     uint32_t tiles_x, hot_rows, hot_n;
-    // 1: the hot slots' waves raise their issue priority (s_setprio), so the frame's longest waves keep
-    // winning VALU arbitration against the younger waves of later frames (RRTE_HOT_PRIO)
-    uint32_t hot_prio;
     uint32_t hot_row_bits[kHotRowWords];
     FrameCam cam[kMaxLaunchFrames];
 };

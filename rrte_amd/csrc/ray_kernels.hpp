@@ -2055,7 +2055,6 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     const uint32_t lane = threadIdx.x & 63u, wave = kWg64 ? 0u : threadIdx.x >> 6;
     const LaunchTile tile = launch_tile(kp);
     if (!tile.run) return;
-    if (kWg64 && kp.hot_prio && blockIdx.z < kp.hot_rows) __builtin_amdgcn_s_setprio(2);
     // frame tile.z of the launch: its camera, its output (multi-frame launches have no f32 output)
     const FrameCam& cm = kp.cam[tile.z];
     if (out_rgba8 && tile.z)

@@ -227,7 +227,6 @@ struct rrte_ctx {
     double split_frac = kSplitFracDefault;  // RRTE_SPLIT_FRAC
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
-    bool env_hot_prio = true;           // RRTE_HOT_PRIO=0: hot slots at the default wave priority (A/B)
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
     struct {
         bool valid = false;
@@ -1129,7 +1128,7 @@ bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
 bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t st) {
     KParams& k = L.k;
     k.tiles_x = L.gx;
-    k.hot_rows = k.hot_n = k.hot_prio = 0;
+    k.hot_rows = k.hot_n = 0;
     k.tile_cost = nullptr;
     k.xterms = nullptr;
     k.xcount = nullptr;
@@ -1167,7 +1166,6 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     if (!tp.slots.empty() && (tp.cur >= 0 || upload_hot_list(c, L.gy))) {
         k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
-        k.hot_prio = c->env_hot_prio ? 1u : 0u;
         k.hot_rows = (k.hot_n + L.gx - 1) / L.gx;
         memcpy(k.hot_row_bits, tp.row_bits, sizeof tp.row_bits);
     }
@@ -1409,7 +1407,6 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         c->env_tile_order_fixed = g[0] == '2';
     }
     if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] == '1';
-    if (const char* g = getenv("RRTE_HOT_PRIO")) c->env_hot_prio = g[0] != '0';
     if (const char* g = getenv("RRTE_SPLIT_FRAC"); g && *g) c->split_frac = strtod(g, nullptr);
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
