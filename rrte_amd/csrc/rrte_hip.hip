@@ -206,6 +206,7 @@ struct rrte_ctx {
         static constexpr int kVersions = 16;
         uint32_t* d_list[kVersions] = {};
         uint32_t* h_list = nullptr;      // pinned staging
+        hipStream_t upload_stream = nullptr;
         int cur = -1;                    // version holding `slots` (-1: not uploaded)
         int next_version = 0;
         uint32_t row_bits[kHotRowWords] = {};
@@ -1096,7 +1097,7 @@ uint32_t split_parts(const rrte_ctx* c, const LaunchPlan& L, uint32_t light_part
 
 // Uploads the composed slots and their tile-row offsets into the next version of the device list
 // (kHotListWords words); false leaves the launch in image order.  The copy completes before any later
-// launch is enqueued (the context's own stream, synchronised), so every launch sees a whole list.
+// launch is enqueued (its own stream, synchronised), so every launch sees a whole list.
 bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
     auto& tp = c->tprof;
     if (tp.next_version == rrte_ctx::TileProfile::kVersions) {
@@ -1116,8 +1117,10 @@ bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
         while (i < tp.slots.size() && hot_y(tp.slots[i]) < y) ++i;
         off[y] = i;
     }
-    if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
+    // a stream of its own: the context's stream may hold a blocking entry point's gather
+    if (!tp.upload_stream && hipStreamCreateWithFlags(&tp.upload_stream, hipStreamNonBlocking) != hipSuccess) return false;
+    if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
+        hipStreamSynchronize(tp.upload_stream) != hipSuccess)
         return false;
     tp.cur = pick;
     return true;
@@ -1471,6 +1474,7 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (c->tprof.d_list[i]) (void)hipFree(c->tprof.d_list[i]);
     }
     if (c->tprof.h_list) (void)hipHostFree(c->tprof.h_list);
+    if (c->tprof.upload_stream) (void)hipStreamDestroy(c->tprof.upload_stream);
     for (auto& xa : c->xarea) {
         if (xa.terms) (void)hipFree(xa.terms);
         if (xa.count) (void)hipFree(xa.count);
