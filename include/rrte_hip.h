@@ -263,7 +263,9 @@ typedef struct rrte_stats {
     double upload_ms;        /* scene H2D time (0 when the scene was cached)   */
     uint64_t frames;         /* frames rendered by this context                */
     uint32_t jit_active;     /* last frame's kernel: 0 generic, 1 full, 2 topology specialisation */
-    uint32_t hot_tiles;      /* tiles the last launch dispatched first (hot-first tile order; 0: image order) */
+    uint32_t hot_tiles;      /* hot slots the last launch dispatched first: the tiles an earlier launch of
+                                the same shape measured slowest (0: image order; env RRTE_TILE_ORDER=0
+                                forces image order).  Never changes a pixel, only when each tile starts. */
     double jit_compile_ms;   /* hiprtc compile time of the last specialised kernel */
 } rrte_stats;
 
