@@ -1912,7 +1912,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
         // publish (agent-scope release fence), count in; the last part to arrive acquires and sums in
         // light order.  (An exchange through uncached memory with atomic stores and loads and no
         // fences was faster and failed one 4K parity run in three: not kept.)
-        __threadfence();
+        if (!(kp.debug & 1024u)) __threadfence();  // RRTE_DEBUG bit 10: no fences (timing only, results may be wrong)
         uint32_t old = 0u;
         if (lane == 0u) old = atomicAdd(sp.count, 1u);
         old = (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
@@ -1920,7 +1920,7 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             sp.skip_store = true;
             return out;
         }
-        __threadfence();
+        if (!(kp.debug & 1024u)) __threadfence();
         if (lane == 0u) __hip_atomic_store(sp.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next use
         if (hit) {
             for (uint32_t li = 0; li < kp.num_lights; ++li) {
