@@ -2193,7 +2193,7 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
         atomicMax(kp.tile_cost + brow * tiles_x + tile.x, (uint32_t)(wall_clock64() - t_wave0));  // tile: its slowest part
     if (stamps && lane == 0) {
         const uint64_t t1 = wall_clock64();
-        const uint32_t wid = (brow * tiles_x + tile.x) * 4u + wave;
+        const uint32_t wid = (brow * tiles_x + tile.x) * 4u + (kWg64 ? tile.part : wave);  // split parts: own slot
         uint32_t* s = reinterpret_cast<uint32_t*>(out_f32) + 4u * wid;
         s[0] = (uint32_t)t_wave0;
         s[1] = (uint32_t)(t_wave0 >> 32);

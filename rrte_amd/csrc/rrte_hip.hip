@@ -1136,7 +1136,9 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     k.xterms = nullptr;
     k.xcount = nullptr;
     memset(k.hot_row_bits, 0, sizeof k.hot_row_bits);
-    if (!c->env_tile_order || c->env_wg256 || L.gy > 32u * kHotRowWords || L.gx > 0xfffu || (k.debug & 48u))
+    // (RRTE_DEBUG bit 5 runs one workgroup in image-order numbering: no tile order; bit 4's per-wave
+    // stamps work with it, a split tile's parts in their own slots)
+    if (!c->env_tile_order || c->env_wg256 || L.gy > 32u * kHotRowWords || L.gx > 0xfffu || (k.debug & 32u))
         return false;
     auto& tp = c->tprof;
     std::string key(reinterpret_cast<const char*>(&kern), sizeof kern);
