@@ -43,6 +43,7 @@ struct LaunchPlan {
     bool cull, single;
     uint32_t num_prims, num_lights, num_materials;
     uint32_t gx, gy;
+    uint32_t cold_rows = 0;  // image-order workgroup rows after the hot rows (gy, or 0 for an LPT list)
 };
 
 constexpr double kSplitFracDefault = 0.7;  // see compose_slots
@@ -205,7 +206,11 @@ struct rrte_ctx {
         // of one stream)
         static constexpr int kVersions = 16;
         uint32_t* d_list[kVersions] = {};
+        size_t cap_list[kVersions] = {};  // words
         uint32_t* h_list = nullptr;      // pinned staging
+        size_t cap_h_list = 0;
+        bool lpt = false;                // RRTE_TILE_ORDER=3: every tile in measured-cost order
+        bool has_split = false;          // some slot of `slots` is a split part
         hipStream_t upload_stream = nullptr;
         int cur = -1;                    // version holding `slots` (-1: not uploaded)
         int next_version = 0;
@@ -228,6 +233,7 @@ struct rrte_ctx {
     double split_frac = kSplitFracDefault;  // RRTE_SPLIT_FRAC
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
+    bool env_tile_order_lpt = false;    // RRTE_TILE_ORDER=3: every tile in measured-cost order (A/B)
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
     struct {
         bool valid = false;
@@ -1031,6 +1037,24 @@ void build_hot_list(rrte_ctx::TileProfile& tp) {
         sum += tp.h_cost[i];
         mx = std::max(mx, tp.h_cost[i]);
     }
+    tp.top_max = mx;
+    if (tp.lpt) {
+        // RRTE_TILE_ORDER=3: every tile, slowest first (longest-processing-time order), by a counting
+        // sort on 65536 cost buckets (ties in tile order): O(tiles) on the host
+        constexpr uint32_t B = 65536;
+        std::vector<uint32_t> cnt(B + 1, 0u);
+        auto bucket = [&](uint32_t c) { return mx ? (uint32_t)((uint64_t)c * (B - 1) / mx) : 0u; };
+        for (uint32_t i = 0; i < n; ++i) ++cnt[B - 1 - bucket(tp.h_cost[i])];
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b <= B; ++b) {
+            const uint32_t c = cnt[b];
+            cnt[b] = acc;
+            acc += c;
+        }
+        tp.top.resize(n);
+        for (uint32_t i = 0; i < n; ++i) tp.top[cnt[B - 1 - bucket(tp.h_cost[i])]++] = {i, tp.h_cost[i]};
+        return;
+    }
     // the candidates above the threshold first (a few percent of the tiles), then a sort of those
     // only: this runs on the host inside a render call (a partial sort over every tile took ~0.7 ms)
     const double thr = std::max(2.0 * sum / n, 0.25 * mx);
@@ -1045,7 +1069,6 @@ void build_hot_list(rrte_ctx::TileProfile& tp) {
         tp.top.resize(kMaxHotTiles);
     }
     std::sort(tp.top.begin(), tp.top.end(), slower);
-    tp.top_max = mx;
 }
 
 // Split tiles: a hot tile at least this fraction of the slowest one (RRTE_SPLIT_FRAC, default 0.7) is
@@ -1058,8 +1081,10 @@ void compose_slots(rrte_ctx::TileProfile& tp, uint32_t parts, uint32_t tiles_x, 
     memset(tp.row_bits, 0, sizeof tp.row_bits);
     tp.slots_parts = parts;
     tp.cur = -1;
+    tp.has_split = false;
     auto add = [&](uint32_t i, uint32_t np) {
         const uint32_t x = i % tiles_x, y = i / tiles_x;
+        tp.has_split |= np > 1;
         for (uint32_t q = 0; q < np; ++q) tp.slots.push_back(hot_pack(x, y, q, np));
         tp.row_bits[y >> 5] |= 1u << (y & 31u);
     };
@@ -1069,6 +1094,16 @@ void compose_slots(rrte_ctx::TileProfile& tp, uint32_t parts, uint32_t tiles_x, 
         uint32_t m = std::min<uint32_t>(tiles, kMaxHotTiles);
         while (m > 1 && (m + 1) / 2 * parts + m / 2 > kMaxHotTiles) --m;
         for (uint32_t j = 0; j < m; ++j) add(m > 1 ? (uint32_t)((uint64_t)j * (tiles - 1) / (m - 1)) : 0u, j % 2 ? 1u : parts);
+    } else if (tp.lpt) {
+        // every tile in cost order; the split ones come first (they are the slowest), and their slots
+        // stay below kMaxHotTiles (the split exchange areas are sized for that many slots)
+        for (const auto& t : tp.top) {
+            uint32_t np = parts > 1 && t.second >= split_frac * tp.top_max ? parts : 1u;
+            if (np > 1 && tp.slots.size() + np > kMaxHotTiles) np = 1u;
+            add(t.first, np);
+        }
+        memset(tp.row_bits, 0, sizeof tp.row_bits);  // no image-order rows follow
+        return;
     } else {
         for (const auto& t : tp.top) {
             const uint32_t np = parts > 1 && t.second >= split_frac * tp.top_max ? parts : 1u;
@@ -1107,15 +1142,33 @@ bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
         tp.next_version = 0;
     }
     const int pick = tp.next_version++;
-    const size_t bytes = kHotListWords * sizeof(uint32_t);
-    if (!tp.d_list[pick] && hipMalloc(reinterpret_cast<void**>(&tp.d_list[pick]), bytes) != hipSuccess) return false;
-    if (!tp.h_list && hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), bytes, hipHostMallocDefault) != hipSuccess) return false;
+    // kHotListWords (slots + row offsets) or, for a whole-frame LPT list, one word per slot
+    const size_t words = std::max<size_t>(kHotListWords, tp.slots.size());
+    const size_t bytes = words * sizeof(uint32_t);
+    if (tp.cap_list[pick] < words) {
+        // a version that may still be read is only ever replaced after the pool's device sync above,
+        // so a larger one for a larger frame needs a sync of its own (rare: a new frame size)
+        if (tp.d_list[pick] && (hipDeviceSynchronize() != hipSuccess || hipFree(tp.d_list[pick]) != hipSuccess)) return false;
+        tp.d_list[pick] = nullptr;
+        tp.cap_list[pick] = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&tp.d_list[pick]), bytes) != hipSuccess) return false;
+        tp.cap_list[pick] = words;
+    }
+    if (tp.cap_h_list < words) {
+        if (tp.h_list) (void)hipHostFree(tp.h_list);
+        tp.h_list = nullptr;
+        tp.cap_h_list = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), bytes, hipHostMallocDefault) != hipSuccess) return false;
+        tp.cap_h_list = words;
+    }
     memset(tp.h_list, 0, bytes);
     memcpy(tp.h_list, tp.slots.data(), tp.slots.size() * sizeof(uint32_t));
-    uint32_t* off = tp.h_list + kMaxHotTiles;
-    for (uint32_t y = 0, i = 0; y <= std::min<uint32_t>(tiles_y, kHotRows); ++y) {
-        while (i < tp.slots.size() && hot_y(tp.slots[i]) < y) ++i;
-        off[y] = i;
+    if (!tp.lpt) {
+        uint32_t* off = tp.h_list + kMaxHotTiles;
+        for (uint32_t y = 0, i = 0; y <= std::min<uint32_t>(tiles_y, kHotRows); ++y) {
+            while (i < tp.slots.size() && hot_y(tp.slots[i]) < y) ++i;
+            off[y] = i;
+        }
     }
     // a stream of its own: the context's stream may hold a blocking entry point's gather
     if (!tp.upload_stream && hipStreamCreateWithFlags(&tp.upload_stream, hipStreamNonBlocking) != hipSuccess) return false;
@@ -1131,6 +1184,7 @@ bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
 bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t st) {
     KParams& k = L.k;
     k.tiles_x = L.gx;
+    L.cold_rows = L.gy;
     k.hot_rows = k.hot_n = 0;
     k.tile_cost = nullptr;
     k.xterms = nullptr;
@@ -1161,6 +1215,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         tp.slots.clear();
         tp.slots_parts = 0;
         tp.fixed = c->env_tile_order_fixed;
+        tp.lpt = c->env_tile_order_lpt;
         tp.launches = kTileReprofile;
     }
     if (tp.fixed) tp.launches = 0;  // RRTE_TILE_ORDER=2: the fixed list, never profiled
@@ -1173,6 +1228,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         k.hot_n = (uint32_t)tp.slots.size();
         k.hot_rows = (k.hot_n + L.gx - 1) / L.gx;
         memcpy(k.hot_row_bits, tp.row_bits, sizeof tp.row_bits);
+        L.cold_rows = tp.lpt ? 0u : L.gy;  // an LPT list covers every tile: no image-order rows
     }
     if (!profile) return false;
     if (ensure(c, tp.d_cost, tp.cap_d, tiles) != RRTE_OK) return false;
@@ -1197,9 +1253,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
 rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& area) {
     area = -1;
     KParams& k = L.k;
-    bool any = false;
-    for (uint32_t i = 0; i < k.hot_n && !any; ++i) any = hot_parts(c->tprof.slots[i]) > 1;
-    if (!any) return RRTE_OK;
+    if (!k.hot_n || !c->tprof.has_split) return RRTE_OK;
     area = c->xnext;
     c->xnext = (c->xnext + 1) % rrte_ctx::kXAreas;
     auto& xa = c->xarea[area];
@@ -1259,7 +1313,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     int area = -1;
     if (rrte_status r = plan_split_area(c, L, st, area); r != RRTE_OK) return r;
     c->stats.hot_tiles = L.k.hot_n;
-    const dim3 grid(L.gx, L.k.nframes, L.k.hot_rows + L.gy), block(kBlockThreads);
+    const dim3 grid(L.gx, L.k.nframes, L.k.hot_rows + L.cold_rows), block(kBlockThreads);
     if (jk) {
         unsigned long long* ctr = c->d_counters;
         MeshView mv = c->mesh_view;
@@ -1410,6 +1464,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
         c->env_tile_order_fixed = g[0] == '2';
+        c->env_tile_order_lpt = g[0] == '3';
     }
     if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] == '1';
     if (const char* g = getenv("RRTE_SPLIT_FRAC"); g && *g) c->split_frac = strtod(g, nullptr);

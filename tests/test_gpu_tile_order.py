@@ -184,3 +184,23 @@ def test_fixed_hot_list_in_batched_gathers(monkeypatch):
         got = o.cpu().numpy().view(np.uint8)
         assert np.array_equal(got, want[i]), f"frame {i}: {(got != want[i]).sum()} bytes differ"
     ctx.close()
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_measured_lpt_order(split, monkeypatch):
+    """RRTE_TILE_ORDER=3: after the profile every tile of the frame is dispatched in measured-cost
+    order (no image-order rows), the slowest ones optionally split; identical to image order."""
+    objs, lights, cam, cfg = scenes.sdf_showcase(480, 272)
+    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    ref = _ctx(monkeypatch, "0", abi.JIT_ON)
+    want = _render(ref, sc, prm)
+    ref.close()
+    ctx = _ctx(monkeypatch, "3", abi.JIT_ON, RRTE_TILE_SPLIT=split)
+    tiles = 60 * 34
+    seen = 0
+    for _ in range(5):
+        got = _render(ctx, sc, prm)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[2]
+        seen = max(seen, got[3])
+    assert seen >= tiles  # every tile has a slot (split parts add more)
+    ctx.close()
