@@ -346,6 +346,14 @@ rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uin
  * 0 = none.  *guards = number of guards.  The program must pass the renderer's validation. */
 rrte_status rrte_hip_sdf_guards(const rrte_sdf_node* in, uint32_t count, uint32_t min_leaves, rrte_sdf_node* out,
                                 uint32_t* guards);
+/* Diagnostic (host only): the hot-first tile order a context would dispatch after a profile with
+ * per-tile durations costs[0..tiles) (tiles_x tiles per row): lpt = 0 the hot list (the up to 1024
+ * slowest tiles of at least twice the mean and a quarter of the slowest, sorted by row then column),
+ * 1 every tile slowest first; parts > 1 splits the tiles of at least split_frac of the slowest into
+ * that many consecutive slots.  Writes *n_slots slots (y << 16 | x << 4 | (parts - 1) << 2 | part)
+ * to slots[0..cap); RRTE_INVALID_ARG if they do not fit. */
+rrte_status rrte_hip_tile_order_plan(const uint32_t* costs, uint32_t tiles, uint32_t tiles_x, int lpt, uint32_t parts,
+                                     double split_frac, uint32_t* slots, uint32_t cap, uint32_t* n_slots);
 
 /* ----------------------------------------------------- multi-GPU (RCCL/xGMI) */
 /* Row-band partition: band b (band_rows rows) belongs to rank b % nranks.

@@ -1663,6 +1663,25 @@ rrte_status rrte_hip_sdf_guards(const rrte_sdf_node* in, uint32_t count, uint32_
     return RRTE_OK;
 }
 
+rrte_status rrte_hip_tile_order_plan(const uint32_t* costs, uint32_t tiles, uint32_t tiles_x, int lpt, uint32_t parts,
+                                     double split_frac, uint32_t* slots, uint32_t cap, uint32_t* n_slots) {
+    if (!costs || !slots || !n_slots || tiles == 0 || tiles_x == 0 || tiles_x > 0xfffu || parts < 1 || parts > 4)
+        return RRTE_INVALID_ARG;
+    rrte_ctx::TileProfile tp;
+    std::vector<uint32_t> h(costs, costs + tiles);
+    tp.h_cost = h.data();
+    tp.tiles = tiles;
+    tp.tiles_x = tiles_x;
+    tp.lpt = lpt != 0;
+    build_hot_list(tp);
+    compose_slots(tp, parts, tiles_x, tiles, split_frac);
+    tp.h_cost = nullptr;  // not owned
+    *n_slots = (uint32_t)tp.slots.size();
+    if (tp.slots.size() > cap) return RRTE_INVALID_ARG;
+    std::copy(tp.slots.begin(), tp.slots.end(), slots);
+    return RRTE_OK;
+}
+
 rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size_t log_len) {
     if (!s || (s->num_prims && !s->prims) || (s->num_sdf_nodes && !s->sdf_nodes)) return RRTE_INVALID_ARG;
     std::vector<DPrim> prims;
