@@ -13,10 +13,7 @@ MAX_SLOTS = 1024
 
 
 def _plan(costs, tiles_x, lpt, parts=1, frac=0.7, cap=None):
-    lib = abi.load()
-    lib.rrte_hip_tile_order_plan.restype = C.c_int
-    lib.rrte_hip_tile_order_plan.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32, C.c_int, C.c_uint32,
-                                              C.c_double, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32)]
+    lib = abi.load()  # (signatures from abi.EXPORTS)
     c = np.ascontiguousarray(costs, dtype=np.uint32)
     cap = cap if cap is not None else len(c) * 4 + 16
     out = np.zeros(cap, dtype=np.uint32)
