@@ -1257,7 +1257,8 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
     area = c->xnext;
     c->xnext = (c->xnext + 1) % rrte_ctx::kXAreas;
     auto& xa = c->xarea[area];
-    const size_t groups = (size_t)k.hot_n * k.nframes;
+    // split groups sit in the first kMaxHotTiles slots (compose_slots), whatever the list's length
+    const size_t groups = (size_t)std::min<uint32_t>(k.hot_n, kMaxHotTiles) * k.nframes;
     const size_t terms = groups * k.num_lights * 3u * 64u;
     if (xa.cap_terms < terms || xa.cap_count < groups) {
         // every area of the ring at once, sized for the

@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_tile_order.py -x -q --timeout 120 --timeout-method thread > gpurun_out/lpt_tests.log 2>&1; tail -1 gpurun_out/lpt_tests.log
 for r in 1 2; do
-  for v in "RRTE_TILE_ORDER=1:RRTE_TILE_SPLIT=0" "RRTE_TILE_ORDER=1:RRTE_TILE_SPLIT=1" "RRTE_TILE_ORDER=3:RRTE_TILE_SPLIT=0" "RRTE_TILE_ORDER=3:RRTE_TILE_SPLIT=1"; do
+  for v in ${VARIANTS:-"RRTE_TILE_ORDER=1:RRTE_TILE_SPLIT=0" "RRTE_TILE_ORDER=1:RRTE_TILE_SPLIT=1" "RRTE_TILE_ORDER=3:RRTE_TILE_SPLIT=0" "RRTE_TILE_ORDER=3:RRTE_TILE_SPLIT=1"}; do
     e="${v//:/ }"
     for st in 200 20; do
       env $e timeout -k 10 200 python -u bench.py --no-cpu --no-stock --steps $st > gpurun_out/lp.log 2>&1 || { tail -5 gpurun_out/lp.log; exit 1; }
