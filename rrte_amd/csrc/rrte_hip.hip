@@ -180,11 +180,12 @@ struct rrte_ctx {
                                  // de-interleave, 4 no comm-stream waits -- results are wrong
     double hp[10] = {};
     uint64_t hp_frames = 0;
-    // Hot-first tile order (KParams::hot).  Every kTileReprofile-th launch of one launch shape (size,
-    // rows, band mapping, mode, kernel) times each tile of its frame 0 on the device and copies the
-    // durations back asynchronously; once they have arrived, later launches of that shape dispatch its
-    // slowest tiles first.  The order never changes a pixel, only when each tile starts.
-    // RRTE_TILE_ORDER=0 turns it off (A/B, tests).
+    // Tile order (KParams::hot).  Every kTileReprofile-th launch of one launch shape (size, rows, band
+    // mapping, mode, kernel) times each tile of its frame 0 on the device and copies the durations back
+    // asynchronously; once they have arrived, later launches of that shape dispatch every tile slowest
+    // first (longest-processing-time order; RRTE_TILE_ORDER=1: only the 1024 slowest first, then image
+    // order).  The order never changes a pixel, only when each tile starts.  RRTE_TILE_ORDER=0 turns it
+    // off (A/B, tests).
     struct TileProfile {
         std::string key;                 // launch shape the hot list belongs to
         std::string pending_key;         // shape of the profile in flight
@@ -233,7 +234,8 @@ struct rrte_ctx {
     double split_frac = kSplitFracDefault;  // RRTE_SPLIT_FRAC
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
-    bool env_tile_order_lpt = false;    // RRTE_TILE_ORDER=3: every tile in measured-cost order (A/B)
+    bool env_tile_order_lpt = true;     // every tile in measured-cost order (default; RRTE_TILE_ORDER=1: the
+                                        // 1024 slowest first, then image order)
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
     struct {
         bool valid = false;
@@ -1465,7 +1467,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
         c->env_tile_order_fixed = g[0] == '2';
-        c->env_tile_order_lpt = g[0] == '3';
+        c->env_tile_order_lpt = g[0] == '3';  // 0 image order, 1 hot list, 2 fixed list (tests), 3 LPT (default)
     }
     if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] == '1';
     if (const char* g = getenv("RRTE_SPLIT_FRAC"); g && *g) c->split_frac = strtod(g, nullptr);
