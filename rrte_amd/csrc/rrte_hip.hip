@@ -232,6 +232,7 @@ struct rrte_ctx {
     int xnext = 0;
     bool env_tile_split = false;       // RRTE_TILE_SPLIT=1: split the slowest hot tiles (measured slower)
     double split_frac = kSplitFracDefault;  // RRTE_SPLIT_FRAC
+    bool env_split_noevent = false;    // RRTE_SPLIT_NOEVENT=1 (timing only): exchange areas reused without events
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
     bool env_tile_order_lpt = true;     // every tile in measured-cost order (default; RRTE_TILE_ORDER=1: the
@@ -1283,6 +1284,12 @@ rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& are
         }
     }
     if (!xa.ev) HIPCHK(c, hipEventCreateWithFlags(&xa.ev, hipEventDisableTiming));
+    if (c->env_split_noevent) {  // RRTE_SPLIT_NOEVENT=1: timing only, the ring is reused untracked
+        k.xterms = xa.terms;
+        k.xcount = xa.count;
+        area = -1;
+        return RRTE_OK;
+    }
     if (xa.used && hipEventQuery(xa.ev) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(st, xa.ev, 0));
     k.xterms = xa.terms;
     k.xcount = xa.count;
@@ -1471,6 +1478,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     }
     if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] == '1';
     if (const char* g = getenv("RRTE_SPLIT_FRAC"); g && *g) c->split_frac = strtod(g, nullptr);
+    if (const char* g = getenv("RRTE_SPLIT_NOEVENT")) c->env_split_noevent = g[0] == '1';
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
