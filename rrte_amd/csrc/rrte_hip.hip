@@ -218,6 +218,7 @@ struct rrte_ctx {
         uint32_t row_bits[kHotRowWords] = {};
         uint64_t launches = 0;           // launches of `key` since its last profile
         uint64_t profiles = 0;           // completed profiles
+        uint64_t cam_sig = 0;            // camera of the last profiled launch (frame 0's FrameCam)
     } tprof;
     // Exchange areas of split tiles (KParams::xterms / xcount), one per launch in a ring; an area is
     // reused after the launch that last used it has completed (else the new launch waits for it)
@@ -1024,6 +1025,13 @@ LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_pa
 
 // Hot-first tile order (rrte_ctx::TileProfile, KParams::hot).
 constexpr uint64_t kTileReprofile = 256;  // launches of one shape between two profiles (each costs a list upload)
+constexpr uint64_t kTileReprofileMoving = 32;  // ... when the camera has moved since the last profile
+
+uint64_t fnv1a(const void* p, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) h = (h ^ static_cast<const unsigned char*>(p)[i]) * 1099511628211ull;
+    return h;
+}
 
 // The slowest tiles of a completed profile: at most kMaxHotTiles, each at least twice the mean tile
 // time and a quarter of the slowest, slowest first.
@@ -1222,7 +1230,10 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         tp.launches = kTileReprofile;
     }
     if (tp.fixed) tp.launches = 0;  // RRTE_TILE_ORDER=2: the fixed list, never profiled
-    const bool profile = !tp.pending && tp.launches >= kTileReprofile;
+    // a moving camera moves the expensive tiles: re-profile after kTileReprofileMoving launches instead
+    const uint64_t cam = fnv1a(&k.cam[0], offsetof(FrameCam, tile_cull));
+    const bool moved = cam != tp.cam_sig;
+    const bool profile = !tp.pending && (tp.launches >= kTileReprofile || (moved && tp.launches >= kTileReprofileMoving));
     ++tp.launches;
     const uint32_t parts = split_parts(c, L, k.light_part);
     if ((!tp.top.empty() || tp.fixed) && (tp.slots_parts != parts || tp.slots.empty())) compose_slots(tp, parts, L.gx, tiles, c->split_frac);
@@ -1246,6 +1257,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     if (!tp.ev && hipEventCreateWithFlags(&tp.ev, hipEventDisableTiming) != hipSuccess) return false;
     if (hipMemsetAsync(tp.d_cost, 0, tiles * sizeof(uint32_t), st) != hipSuccess) return false;  // atomicMax per tile
     k.tile_cost = tp.d_cost;
+    tp.cam_sig = cam;
     tp.pending_key = key;
     tp.tiles = tiles;
     tp.tiles_x = L.gx;
