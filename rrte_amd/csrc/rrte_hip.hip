@@ -48,6 +48,18 @@ struct LaunchPlan {
 
 constexpr double kSplitFracDefault = 0.7;  // see compose_slots
 
+// A tile order composed off the render thread (plan_tile_order): the profile's shape key, the measured
+// tiles in dispatch priority and the slot list for `parts` parts per split tile.
+struct TilePlanResult {
+    std::string key;
+    std::vector<std::pair<uint32_t, uint32_t>> top;
+    uint32_t top_max = 0;
+    std::vector<uint32_t> slots;
+    uint32_t row_bits[kHotRowWords] = {};
+    bool has_split = false;
+    uint32_t parts = 0;
+};
+
 struct rrte_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -219,6 +231,8 @@ struct rrte_ctx {
         uint64_t launches = 0;           // launches of `key` since its last profile
         uint64_t profiles = 0;           // completed profiles
         uint64_t cam_sig = 0;            // camera of the last profiled launch (frame 0's FrameCam)
+        std::future<TilePlanResult> work;  // composition of the last profile's order (worker thread)
+        bool working = false;
     } tprof;
     // Exchange areas of split tiles (KParams::xterms / xcount), one per launch in a ring; an area is
     // reused after the launch that last used it has completed (else the new launch waits for it)
@@ -1141,6 +1155,28 @@ uint32_t split_parts(const rrte_ctx* c, const LaunchPlan& L, uint32_t light_part
     return parts;
 }
 
+// Allocates what an upload of up to `words` list words needs -- pinned staging, the upload stream and
+// the device versions not yet allocated -- at profile time, so the first upload (inside a later render
+// call) allocates nothing.
+bool reserve_hot_lists(rrte_ctx* c, size_t words) {
+    auto& tp = c->tprof;
+    if (tp.cap_h_list < words) {
+        if (tp.h_list) (void)hipHostFree(tp.h_list);
+        tp.h_list = nullptr;
+        tp.cap_h_list = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), words * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+            return false;
+        tp.cap_h_list = words;
+    }
+    if (!tp.upload_stream && hipStreamCreateWithFlags(&tp.upload_stream, hipStreamNonBlocking) != hipSuccess) return false;
+    for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i)
+        if (!tp.d_list[i]) {
+            if (hipMalloc(reinterpret_cast<void**>(&tp.d_list[i]), words * sizeof(uint32_t)) != hipSuccess) return false;
+            tp.cap_list[i] = words;
+        }
+    return true;
+}
+
 // Uploads the composed slots and their tile-row offsets into the next version of the device list
 // (kHotListWords words); false leaves the launch in image order.  The copy completes before any later
 // launch is enqueued (its own stream, synchronised), so every launch sees a whole list.
@@ -1211,13 +1247,53 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
                               (uint32_t)L.mode, (uint32_t)L.cull, (uint32_t)L.single};
     key.append(reinterpret_cast<const char*>(shape), sizeof shape);
     const uint32_t tiles = L.gx * L.gy;
+    const uint32_t parts = split_parts(c, L, k.light_part);
     if (tp.pending && hipEventQuery(tp.ev) == hipSuccess) {
         tp.pending = false;
         if (tp.pending_key == key) {
-            build_hot_list(tp);
-            tp.key = key;
+            // the order is composed on a worker thread from a copy of the durations: a whole frame's
+            // counting sort and slot list take ~0.5 ms of host time that a render call must not stall for
+            std::vector<uint32_t> costs(tp.h_cost, tp.h_cost + tp.tiles);
+            const uint32_t n = tp.tiles, tx = tp.tiles_x;
+            const bool lpt = tp.lpt;
+            const double frac = c->split_frac;
+            tp.work = std::async(std::launch::async, [key, costs = std::move(costs), n, tx, lpt, parts, frac]() {
+                rrte_ctx::TileProfile w;
+                w.h_cost = const_cast<uint32_t*>(costs.data());
+                w.tiles = n;
+                w.tiles_x = tx;
+                w.lpt = lpt;
+                build_hot_list(w);
+                compose_slots(w, parts, tx, n, frac);
+                TilePlanResult r;
+                r.key = key;
+                r.top = std::move(w.top);
+                r.top_max = w.top_max;
+                r.slots = std::move(w.slots);
+                memcpy(r.row_bits, w.row_bits, sizeof r.row_bits);
+                r.has_split = w.has_split;
+                r.parts = parts;
+                w.h_cost = nullptr;
+                return r;
+            });
+            tp.working = true;
             tp.launches = 0;
             ++tp.profiles;
+        }
+    }
+    if (tp.working && tp.work.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
+        TilePlanResult r = tp.work.get();
+        tp.working = false;
+        if (r.key == key) {  // (a result for another shape is dropped)
+            tp.key = key;
+            tp.top = std::move(r.top);
+            tp.top_max = r.top_max;
+            tp.slots = std::move(r.slots);
+            memcpy(tp.row_bits, r.row_bits, sizeof tp.row_bits);
+            tp.has_split = r.has_split;
+            tp.slots_parts = r.parts;
+            tp.fixed = false;
+            tp.cur = -1;
         }
     }
     if (tp.key != key) {  // another shape: drop the list, profile as soon as the copy buffer is free
@@ -1235,7 +1311,6 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     const bool moved = cam != tp.cam_sig;
     const bool profile = !tp.pending && (tp.launches >= kTileReprofile || (moved && tp.launches >= kTileReprofileMoving));
     ++tp.launches;
-    const uint32_t parts = split_parts(c, L, k.light_part);
     if ((!tp.top.empty() || tp.fixed) && (tp.slots_parts != parts || tp.slots.empty())) compose_slots(tp, parts, L.gx, tiles, c->split_frac);
     if (!tp.slots.empty() && (tp.cur >= 0 || upload_hot_list(c, L.gy))) {
         k.hot = tp.d_list[tp.cur];
@@ -1255,6 +1330,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         tp.cap_h = tiles;
     }
     if (!tp.ev && hipEventCreateWithFlags(&tp.ev, hipEventDisableTiming) != hipSuccess) return false;
+    if (!reserve_hot_lists(c, std::max<size_t>(kHotListWords, (size_t)tiles + kMaxHotTiles))) return false;
     if (hipMemsetAsync(tp.d_cost, 0, tiles * sizeof(uint32_t), st) != hipSuccess) return false;  // atomicMax per tile
     k.tile_cost = tp.d_cost;
     tp.cam_sig = cam;
