@@ -71,6 +71,23 @@ int main() {
     CHECK(rrte_hip_jit_check(nullptr, 1, nullptr, 0) == RRTE_INVALID_ARG, "jit_check null");
     CHECK(rrte_hip_band_rows_for_rank(1080, 16, 8, 3) == 136u, "band rows (8 full bands + the 8-row last)");
     CHECK(rrte_hip_band_rows_for_rank(1080, 16, 8, 7) == 128u, "band rows last rank");
+    {
+        // tile-order planning (the host code a context runs after a profile): hot list and LPT, with
+        // and without split tiles, on a 240 x 135 frame with a silhouette-like tail
+        const uint32_t tx = 240, n = 240 * 135;
+        std::vector<uint32_t> costs(n), slots(n + 2048);
+        for (uint32_t i = 0; i < n; ++i) costs[i] = 200u + (i * 2654435761u >> 20) % 3000u + (i % 97 == 0 ? 9000u : 0u);
+        for (int lpt = 0; lpt < 2; ++lpt)
+            for (uint32_t parts : {1u, 3u}) {
+                uint32_t got = 0;
+                CHECK(rrte_hip_tile_order_plan(costs.data(), n, tx, lpt, parts, 0.7, slots.data(), (uint32_t)slots.size(),
+                                               &got) == RRTE_OK, "tile order plan");
+                CHECK(lpt ? got >= n : (got > 0 && got <= 1024u), "tile order slot count %u", got);
+            }
+        uint32_t got = 0;
+        CHECK(rrte_hip_tile_order_plan(costs.data(), n, tx, 1, 1, 0.7, slots.data(), 16, &got) == RRTE_INVALID_ARG,
+              "tile order plan into a small buffer");
+    }
     try {
         twist(Vec3(1.0f, 1.0f, 0.0f), 1.0f);
         CHECK(false, "non-axis deformer accepted");
