@@ -93,12 +93,12 @@ def cpu_baseline(scene, params, budget_s, stock=None):
 
     threads = cpu_threads()
     W, H = params.width, params.height
-    oracle.render(scene, params, nthreads=threads, want_f32=False)  # warm-up
+    frame8, _, _ = oracle.render(scene, params, nthreads=threads, want_f32=False)  # warm-up
     times, shadow = [], 0
     t_start = time.perf_counter()
     while len(times) < 5:
         t0 = time.perf_counter()
-        _, _, shadow = oracle.render(scene, params, nthreads=threads, want_f32=False)
+        frame8, _, shadow = oracle.render(scene, params, nthreads=threads, want_f32=False)
         times.append(time.perf_counter() - t0)
         if time.perf_counter() - t_start > budget_s:
             break
@@ -126,7 +126,31 @@ def cpu_baseline(scene, params, budget_s, stock=None):
         ts = time.perf_counter() - t0
         out["stock_config"] = {"value": W * (band[1] - band[0]) * sprm.samples_per_pixel / ts / 1e6,
                                "unit": "Msample/s", "cores": threads, "rows": list(band)}
-    return out
+    return out, (frame8, shadow)
+
+
+def oracle_frame(scene, params):
+    """The oracle's RGBA8 frame and shadow-ray count (the verification reference when the CPU baseline
+    leg does not run: N > 1, --no-cpu)."""
+    import oracle
+
+    out8, _, shadow = oracle.render(scene, params, nthreads=cpu_threads(), want_f32=False)
+    return out8, shadow
+
+
+def verify_frames(frames_u8, timed_shadow, steps, ref):
+    """The timed frames against the oracle: every buffer in flight holds the last
+    timed frame rendered into it; compared byte for byte with the oracle's RGBA8 frame of the same
+    scene and parameters (the device gamma byte is proven identical to its powf path; glibc's powf
+    may differ by an ulp, hence u8 max diff <= 1 as the bar), and the timed frames' shadow-ray total
+    with steps x the oracle's count (exact)."""
+    ref8, ref_shadow = ref
+    diffs = [np.abs(f.astype(np.int16) - ref8.astype(np.int16)) for f in frames_u8]
+    return {"frames": len(frames_u8), "u8_max_diff": int(max(int(d.max()) for d in diffs)),
+            "bytes_differing": int(sum(int((d != 0).sum()) for d in diffs)),
+            "shadow_rays_match": int(timed_shadow) == steps * int(ref_shadow),
+            "shadow_rays_per_frame": {"timed_mean": timed_shadow / steps, "oracle": int(ref_shadow)},
+            "reference": "oracle/rrte_oracle.c (C restatement of Raytracer::render), same scene and parameters"}
 
 
 def flop_tally(scene, params):
@@ -344,6 +368,8 @@ def main():
     ctx.check(lib.rrte_hip_synchronize(ctx.h))
     st = ctx.stats()
     elapsed = t1 - t0
+    # the timed frames themselves, for the verification against the oracle (outside the timed region)
+    timed_frames = [f.cpu().numpy().view(np.uint8).copy() for f in fulls[:min(F, args.steps)]] if rank == 0 else []
     rows = lib.rrte_hip_band_rows_for_rank(H, args.band_rows, world, rank) if dist_on else H
     primary = W * rows * prm.samples_per_pixel * args.steps
     shadow = int(st.shadow_rays)
@@ -436,8 +462,11 @@ def main():
         avg_launch_ms = b2b_ms
         # algorithmic HBM bytes per launch: the RGBA8 framebuffer store, 4 B per pixel;
         # the scene (<= a few KB) is served from the scalar cache and counts once.
-        bytes_per_launch = 4 * W * H
+        bytes_per_launch = 4 * W * rows
         achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+        flops_frame, _, _ = flop_tally(scene, prm)
+        flops_launch = flops_frame * rows / H
+        valu_tf = flops_launch / (avg_launch_ms * 1e-3) / 1e12
         wl = f"{args.scene}@{W}x{H}/{args.mode}"
         pmc = pmc_traffic(wl)
         line = {
@@ -466,13 +495,20 @@ def main():
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "parallelism": f"rows{world}" if world > 1 else "single",
             },
+            # the binding roofline: VALU FP32 (no dense contraction, no MFMA).  achieved =
+            # algorithmic FP32 ops of one launch (the oracle's instrumented counting build) / the
+            # average launch duration; HBM beside it (4 B/pixel frame store, PMC traffic)
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 3),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
+                "bound": "valu",
+                "achieved": round(valu_tf, 3),
+                "peak": VALU_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": valu_tf / VALU_PEAK_TFLOPS,
                 "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/pmc_*.json)",
+                "flops_per_launch": flops_launch,
+                "frac_of_unpacked_peak": valu_tf / (VALU_PEAK_TFLOPS / 2),
+                "achieved_at_frame_rate": round(flops_launch / (elapsed / args.steps) / 1e12, 3),
                 "kernel": ("rrte_jit_kernel (scene-specialised, hiprtc)" if st.jit_active else
                            "rrte::ray_kernel<%s> (generic)" % ("LAMBERT_SHADOW" if args.mode == "lambert_shadow" else "REFCOMPAT")),
                 "jit_compile_ms": round(st.jit_compile_ms, 1) if st.jit_active else None,
@@ -482,15 +518,23 @@ def main():
                 "avg_launch_note": f"HIP events around {n_seq} frames run back to back on one stream, span / {n_seq}; "
                                    "launch_ms_each: an event pair around each frame (includes the stream gap)",
                 "launch_ms_each": [round(x, 4) for x in launch_ms],
-                "bytes_per_launch": bytes_per_launch,
-                "note": "VALU-bound path (no dense contraction, no MFMA); HBM traffic is the 4 B/pixel frame store",
+                "note": "peak = packed-FP32 vector peak (MI355X_MICROARCH.md); the kernel issues unpacked FP32, one ray "
+                        "per lane" + ("" if world == 1 else f"; N > 1: rank 0's share, flops scaled by its rows ({rows}/{H})"),
+                "hbm": {"achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": bytes_per_launch,
+                        "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                        "note": "algorithmic bytes = the 4 B/pixel RGBA8 frame store"},
             },
         }
         line["primary_only"] = {"value": round(primary / elapsed / 1e6, 3), "unit": "Mray/s"}
         line["frame_latency_ms"] = round(latency_ms, 4)
         line["host_enqueue_ms_per_step"] = round((t_enq - t0) / args.steps * 1e3, 4)
         # hot-first tile order: slots of the timed frames' launches dispatched first
-        line["tile_order"] = {"hot_slots": int(st.hot_tiles), "env": os.environ.get("RRTE_TILE_ORDER", "1")}
+        env_order = os.environ.get("RRTE_TILE_ORDER", "")
+        line["tile_order"] = {"hot_slots": int(st.hot_tiles),
+                              "tiles": ((W + 7) // 8) * ((rows + 7) // 8),
+                              "mode": {"0": "image order", "2": "fixed permutation (tests)"}.get(
+                                  env_order, "measured cost, slowest first (default)")}
         line["d2h_ms"] = round(d2h_ms, 4)  # frame to pinned host memory, excluded from `value`
         if pmc and pmc.get("valu") is not None:
             line["valu"] = dict(pmc["valu"])
@@ -517,21 +561,15 @@ def main():
         if stock is not None:
             line["stock_config"] = stock
         if world == 1 and not args.no_cpu:
-            flops, _, _ = flop_tally(scene, prm)
-            tf = flops / (avg_launch_ms * 1e-3) / 1e12
-            line["valu_roofline"] = {
-                "bound": "valu-fp32", "flops_per_frame": flops, "achieved": round(tf, 3), "unit": "TFLOP/s",
-                "peak": VALU_PEAK_TFLOPS, "frac": tf / VALU_PEAK_TFLOPS,
-                "frac_of_unpacked_peak": tf / (VALU_PEAK_TFLOPS / 2),
-                "achieved_at_frame_rate": round(flops / (elapsed / args.steps) / 1e12, 3),
-                "note": "algorithmic FP32 ops from the oracle's instrumented counting build (SURVEY §8d) / "
-                        "avg kernel duration; peak = packed-FP32 vector peak (the kernel issues unpacked FP32)"}
             sband = (H // 2 - H // 8, H // 2 + H // 8)  # centre quarter of the frame
-            line["cpu_baseline"] = cpu_baseline(scene, prm, args.cpu_seconds,
-                                                stock=(*stock_config(args), sband) if stock else None)
+            line["cpu_baseline"], ref = cpu_baseline(scene, prm, args.cpu_seconds,
+                                                     stock=(*stock_config(args), sband) if stock else None)
             line["cpu_baseline"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 2)
             if stock and "stock_config" in line["cpu_baseline"]:
                 line["stock_config"]["gpu_over_cpu"] = round(stock["value"] / line["cpu_baseline"]["stock_config"]["value"], 2)
+        else:
+            ref = oracle_frame(scene, prm)
+        line["verified"] = verify_frames(timed_frames, shadow, args.steps, ref)  # (shadow: summed over ranks)
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist_on:

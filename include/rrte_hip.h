@@ -293,7 +293,10 @@ rrte_status rrte_hip_render_f32(rrte_ctx* ctx, const rrte_scene_ir* scene,
  * one frame on `stream` (a hipStream_t, or null for the context's stream)
  * writing to device buffers (either may be null).  Returns without
  * synchronising; shadow-ray counts accumulate on the device and are folded
- * into rrte_hip_stats at the next synchronising call. */
+ * into rrte_hip_stats at the next synchronising call.  A stream passed here (or to
+ * rrte_hip_render_gather_async) must stay valid until the next rrte_hip_synchronize: the context
+ * records events on it when a scene or tile-list version it read is retired.  Scene changes never
+ * drain the device: the scene is kept in a ring of versions. */
 rrte_status rrte_hip_render_async(rrte_ctx* ctx, const rrte_scene_ir* scene,
                                   const rrte_render_params* params, void* d_out_rgba8,
                                   void* d_out_rgba32f, void* stream);
@@ -346,14 +349,17 @@ rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uin
  * 0 = none.  *guards = number of guards.  The program must pass the renderer's validation. */
 rrte_status rrte_hip_sdf_guards(const rrte_sdf_node* in, uint32_t count, uint32_t min_leaves, rrte_sdf_node* out,
                                 uint32_t* guards);
-/* Diagnostic (host only): the hot-first tile order a context would dispatch after a profile with
- * per-tile durations costs[0..tiles) (tiles_x tiles per row): lpt = 0 the hot list (the up to 1024
- * slowest tiles of at least twice the mean and a quarter of the slowest, sorted by row then column),
- * 1 every tile slowest first; parts > 1 splits the tiles of at least split_frac of the slowest into
- * that many consecutive slots.  Writes *n_slots slots (y << 16 | x << 4 | (parts - 1) << 2 | part)
- * to slots[0..cap); RRTE_INVALID_ARG if they do not fit. */
-rrte_status rrte_hip_tile_order_plan(const uint32_t* costs, uint32_t tiles, uint32_t tiles_x, int lpt, uint32_t parts,
-                                     double split_frac, uint32_t* slots, uint32_t cap, uint32_t* n_slots);
+/* Diagnostic (host only): the measured-cost tile order a context dispatches after a profile with
+ * per-tile durations costs[0..tiles) (tiles_x tiles per row): every tile once, slowest first (a
+ * counting sort on 65536 cost buckets, ties in tile order).  Writes *n_slots = tiles slots
+ * (y << 16 | x) to slots[0..cap); RRTE_INVALID_ARG if they do not fit. */
+rrte_status rrte_hip_tile_order_plan(const uint32_t* costs, uint32_t tiles, uint32_t tiles_x, uint32_t* slots,
+                                     uint32_t cap, uint32_t* n_slots);
+/* Diagnostic (host only): the persistent JIT cache's file name (32 hex digits + NUL, out_len >= 33)
+ * for a generated kernel `source`: a hash of the source, the device headers embedded in this library
+ * (or `headers_override` in their place, to show that a rebuilt library's headers change the key),
+ * the hiprtc options (RRTE_JIT_EXTRA_OPTS included) and the hiprtc version. */
+rrte_status rrte_hip_jit_cache_key(const char* source, const char* headers_override, char* out, size_t out_len);
 
 /* ----------------------------------------------------- multi-GPU (RCCL/xGMI) */
 /* Row-band partition: band b (band_rows rows) belongs to rank b % nranks.

@@ -77,21 +77,11 @@ struct FrameCam {
 // cameras (blockIdx.y = frame; batched multi-GPU frames, rrte_hip_set_gather_batch).
 constexpr uint32_t kMaxLaunchFrames = 8;
 
-// Hot-first tile order (KParams::hot): at most this many hot slots, and tile rows < 32 * kHotRowWords
-// (4096 pixels) per launch.  A slot is packed y << 16 | x << 4 | (parts - 1) << 2 | part (x < 4096):
-// a split tile (parts > 1, at most 4) takes `parts` consecutive slots, each rendering the tile's
-// camera rays and the shadow rays of the lights KParams::light_part gives that part.
-// The slots live in device memory (KParams::hot): kMaxHotTiles slots, then kHotRows + 1 tile-row
-// offsets (the slots of tile row y are [off[y], off[y + 1])).
-constexpr uint32_t kMaxHotTiles = 1024, kHotRowWords = 16, kHotRows = 32 * kHotRowWords, kMaxSplitLights = 64;
-constexpr uint32_t kHotListWords = kMaxHotTiles + kHotRows + 1;
-__host__ __device__ constexpr uint32_t hot_pack(uint32_t x, uint32_t y, uint32_t part, uint32_t parts) {
-    return (y << 16) | (x << 4) | ((parts - 1u) << 2) | part;
-}
-__host__ __device__ constexpr uint32_t hot_x(uint32_t h) { return (h >> 4) & 0xfffu; }
+// Measured-cost tile order (KParams::hot): slot k of a launch renders the tile packed in hot[k] as
+// y << 16 | x (tile columns and rows < 65536).  A list covers every tile of the launch shape once.
+__host__ __device__ constexpr uint32_t hot_pack(uint32_t x, uint32_t y) { return (y << 16) | x; }
+__host__ __device__ constexpr uint32_t hot_x(uint32_t h) { return h & 0xffffu; }
 __host__ __device__ constexpr uint32_t hot_y(uint32_t h) { return h >> 16; }
-__host__ __device__ constexpr uint32_t hot_part(uint32_t h) { return h & 3u; }
-__host__ __device__ constexpr uint32_t hot_parts(uint32_t h) { return ((h >> 2) & 3u) + 1u; }
 
 // Per-launch constants, passed by value (kernel arguments land in SGPRs).
 struct KParams {
@@ -109,23 +99,18 @@ struct KParams {
     uint32_t debug;          // RRTE_DEBUG ablation bits (diagnostics only, 0 in production)
     uint32_t nframes;        // frames of this launch (gridDim.y), cam[0 .. nframes)
     uint64_t frame_stride;   // bytes between consecutive frames' RGBA8 / slab outputs
-    // Tile order of 64-thread-workgroup launches: grid (tiles_x, nframes, hot_rows + tile rows).
-    // Workgroup rows [0, hot_rows) render the hot slots hot[0 .. hot_n) of every frame first -- the
-    // tiles the context measured slowest on an earlier frame (rrte_hip.hip, TileProfile) -- and the
-    // image-order workgroup of a hot tile exits (its row has a bit in hot_row_bits).  Pixels are
+    // Tile order of 64-thread-workgroup launches: grid (tiles_x, nframes, tile rows).  With a list
+    // (hot != nullptr) workgroup slot k = blockIdx.z * tiles_x + blockIdx.x renders tile hot[k] of its
+    // frame -- every tile, slowest first as an earlier launch of the same shape measured them
+    // (rrte_hip.hip, TileProfile); without one, tile (blockIdx.x, blockIdx.z).  Pixels are
     // independent (raytracer.rs:57-60), so any order renders the same bytes; this one starts the
     // frame's longest waves first instead of wherever image order puts them.
     uint32_t* tile_cost;     // non-null: frame 0's workgroups store their duration (100 MHz ticks) at [y * tiles_x + x]
-    // Split hot tiles (LAMBERT_SHADOW, one sample): each part publishes its lights' terms for every
-    // lane into xterms (block (first slot * nframes + frame) of num_lights * 3 * 64 floats) and counts
-    // itself in xcount; the last part to arrive sums every light's term in light order -- the
-    // reference's accumulation order (raytracer.rs ray_color) -- and writes the pixels.
-    float* xterms;
-    uint32_t* xcount;
-    uint32_t light_part[kMaxSplitLights / 16];  // 2 bits per light: the part that shades it
-    const uint32_t* hot;     // device hot list (kHotListWords words; immutable while launches use it)
-    uint32_t tiles_x, hot_rows, hot_n;
-    uint32_t hot_row_bits[kHotRowWords];
+    const uint32_t* hot;     // device tile list (hot_n words; immutable while launches use it)
+    uint32_t tiles_x, hot_n;
+    // Output rows: 0 = this launch's rows packed (row r at r * width), 1 = at their image rows
+    // (image_row(r) * width: a multi-GPU root renders its own bands straight into the final frame)
+    uint32_t out_image_rows;
     FrameCam cam[kMaxLaunchFrames];
 };
 static_assert(sizeof(KParams) <= 3584, "kernel arguments stay below the 4 KB kernarg limit");

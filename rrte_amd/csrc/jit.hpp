@@ -58,4 +58,8 @@ void jit_release(JitKernel& k);
 // hiprtc compile only (no module load, no device needed): diagnostics / CPU tests.
 bool jit_compile_only(const std::string& src, std::string& log);
 
+// The persistent cache's file name for `src` (32 hex digits): a hash of the source, the embedded
+// device headers (or `hdr_override` in their place, tests), the hiprtc options and version.
+std::string jit_cache_name(const std::string& src, const char* hdr_override);
+
 }  // namespace rrte

@@ -1765,26 +1765,10 @@ __device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray
 // LAMBERT_SHADOW (build-defined) for one camera ray.  Called by
 // all 64 lanes of the wave (`live` marks the lanes that own a pixel): with
 // CULL the hit-point bound and the per-light shadow culls are wave reductions.
-// Exchange block of a split tile (KParams::xterms): [light][channel][64 lanes] floats, and its
-// arrival counter.
-struct TileSplit {
-    uint32_t part, parts;
-    float* terms;
-    uint32_t* count;
-    bool skip_store;  // set by shade_lambert for every part but the last to arrive
-};
-__device__ __forceinline__ uint32_t light_part(const KParams& kp, uint32_t li) {
-    return (kp.light_part[(li >> 4) & 3u] >> ((li & 15u) * 2u)) & 3u;
-}
-
 constexpr bool kShadeAll = RRTE_MARCH_PRED >= 3;  // shade every lane (predicated), or only hit lanes
-// A split tile's part (sp.parts > 1) shades only its own lights, publishing each light's term
-// (+0 when the light adds nothing: c + 0 == c here, as c = 0 + albedo * 0.01 is never -0 and RN sums
-// of non-(-0) operands are never -0) for the last part to arrive, which adds them in light order and
-// returns the pixel; the other parts return with sp.skip_store set.
 template <class S, bool CULL>
 __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, const Cull& cl, const Ray& r, bool live,
-                                             uint32_t& nshadow, uint32_t pmask, TileSplit& sp) {
+                                             uint32_t& nshadow, uint32_t pmask) {
     Col out{0.0f, 0.0f, 0.0f, 1.0f};
     if (kp.max_depth == 0) return out;
     Hit h;
@@ -1814,27 +1798,16 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
     const float bias = kp.bias;
     // contribution of one light to a hit lane (light.rs illuminate + N.L + shadow ray)
     // RRTE_DEBUG bit 8 (timing diagnostics only, wrong images): shadow tests for light (debug >> 9) & 7 only
-    const bool split = sp.parts > 1u;
-    const uint32_t lane = threadIdx.x & 63u;
-    auto publish = [&](uint32_t li, float tr, float tg, float tb) {
-        sp.terms[(li * 3u + 0u) * 64u + lane] = tr;
-        sp.terms[(li * 3u + 1u) * 64u + lane] = tg;
-        sp.terms[(li * 3u + 2u) * 64u + lane] = tb;
-    };
     auto shade = [&](const DLight& l, uint64_t smask, uint32_t li) {
-        if (split && light_part(kp, li) != sp.part) return;  // another part's light
         Contrib k = illuminate(l, h.p);
         if (l.kind == RRTE_LIGHT_AMBIENT) {
-            if (split) {
-                publish(li, ar * k.cr, ag * k.cg, ab * k.cb);
-            } else if (hit) {
+            if (hit) {
                 cr = cr + ar * k.cr;
                 cg = cg + ag * k.cg;
                 cb = cb + ab * k.cb;
             }
             return;
         }
-        float tr = 0.0f, tg = 0.0f, tb = 0.0f;  // split: this light's term
         const float ndl = vdot(h.n, k.dir);
 #if RRTE_MARCH_PRED >= 3
         // predicated over every lane (hit or not): a lane that casts no shadow ray tests the empty
@@ -1847,15 +1820,9 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             const bool occ = !skip && occluded(sc, sr, bias, cast ? k.dist : -kInf, smask, (kp.debug & 64u) ? idx : -1);
             if (cast && !occ) {
                 float f = k.att * ndl;
-                if (split) {
-                    tr = ar * (k.cr * f);
-                    tg = ag * (k.cg * f);
-                    tb = ab * (k.cb * f);
-                } else {
-                    cr = cr + ar * (k.cr * f);
-                    cg = cg + ag * (k.cg * f);
-                    cb = cb + ab * (k.cb * f);
-                }
+                cr = cr + ar * (k.cr * f);
+                cg = cg + ag * (k.cg * f);
+                cb = cb + ab * (k.cb * f);
             }
         }
         if (false) {
@@ -1868,18 +1835,11 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             if ((kp.debug & 1u) || ((kp.debug & 256u) && li != ((kp.debug >> 9) & 7u)) ||
                 !occluded(sc, sr, bias, k.dist, smask, (kp.debug & 64u) ? idx : -1)) {
                 float f = k.att * ndl;
-                if (split) {
-                    tr = ar * (k.cr * f);
-                    tg = ag * (k.cg * f);
-                    tb = ab * (k.cb * f);
-                } else {
-                    cr = cr + ar * (k.cr * f);
-                    cg = cg + ag * (k.cg * f);
-                    cb = cb + ab * (k.cb * f);
-                }
+                cr = cr + ar * (k.cr * f);
+                cg = cg + ag * (k.cg * f);
+                cb = cb + ab * (k.cb * f);
             }
         }
-        if (split) publish(li, tr, tg, tb);
     };
     if constexpr (!CULL) {
         if (kShadeAll || hit) for_each_light(sc, [&](auto lii) { shade(light_at(sc, lii), ~0ull, (uint32_t)lii); });
@@ -1905,28 +1865,6 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             for (uint32_t li = 0; li < sc.num_lights; ++li) {
                 const uint64_t sm = shadow_cull(cl, hb, sc.lights[li], bnd);
                 if (kShadeAll || hit) shade(sc.lights[li], sm, li);
-            }
-        }
-    }
-    if (split) {
-        // publish (agent-scope release fence), count in; the last part to arrive acquires and sums in
-        // light order.  (An exchange through uncached memory with atomic stores and loads and no
-        // fences was faster and failed one 4K parity run in three: not kept.)
-        if (!(kp.debug & 1024u)) __threadfence();  // RRTE_DEBUG bit 10: no fences (timing only, results may be wrong)
-        uint32_t old = 0u;
-        if (lane == 0u) old = atomicAdd(sp.count, 1u);
-        old = (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
-        if (old + 1u != sp.parts) {
-            sp.skip_store = true;
-            return out;
-        }
-        if (!(kp.debug & 1024u)) __threadfence();
-        if (lane == 0u) __hip_atomic_store(sp.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next use
-        if (hit) {
-            for (uint32_t li = 0; li < kp.num_lights; ++li) {
-                cr = cr + sp.terms[(li * 3u + 0u) * 64u + lane];
-                cg = cg + sp.terms[(li * 3u + 1u) * 64u + lane];
-                cb = cb + sp.terms[(li * 3u + 2u) * 64u + lane];
             }
         }
     }
@@ -2002,46 +1940,21 @@ __device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp, const Fr
     return m | (cm.tile_n < 32u ? (~0u << cm.tile_n) : 0u);  // objects past the table: never culled
 }
 
-// The tile (x, y in workgroup units) and frame of this workgroup (KParams::hot, hot-first order);
-// run = false for an unused hot slot and for the image-order workgroup of a hot tile.  A split hot
-// tile (parts > 1) occupies `parts` consecutive hot slots from `slot`; this workgroup is its `part`.
-struct LaunchTile { uint32_t x, y, z; bool run; uint32_t part, parts, slot; };
+// The tile (x, y in workgroup units) and frame of this workgroup: with a tile list (KParams::hot,
+// measured-cost order) slot k = blockIdx.z * tiles_x + blockIdx.x renders tile hot[k] (a wave-uniform
+// index: one scalar load); run = false for the unused slots of the last slot row.
+struct LaunchTile { uint32_t x, y, z; bool run; };
 __device__ __forceinline__ LaunchTile launch_tile(const KParams& kp) {
-    if (!kWg64) return LaunchTile{blockIdx.x, blockIdx.y, blockIdx.z, true, 0u, 1u, 0u};
-    LaunchTile t{blockIdx.x, 0u, blockIdx.y, true, 0u, 1u, 0u};
-    const uint32_t r = blockIdx.z;
-    if (r < kp.hot_rows) {  // hot slot k: wave-uniform index, a scalar load
-        const uint32_t k = r * kp.tiles_x + blockIdx.x;
+    if (!kWg64) return LaunchTile{blockIdx.x, blockIdx.y, blockIdx.z, true};
+    LaunchTile t{blockIdx.x, blockIdx.z, blockIdx.y, true};
+    if (kp.hot) {
+        const uint32_t k = blockIdx.z * kp.tiles_x + blockIdx.x;
         t.run = k < kp.hot_n;
         const uint32_t h = kp.hot[t.run ? k : 0u];
         t.x = hot_x(h);
         t.y = hot_y(h);
-        t.part = hot_part(h);
-        t.parts = hot_parts(h);
-        t.slot = k - t.part;
-        return t;
-    }
-    t.y = r - kp.hot_rows;
-    if ((kp.hot_row_bits[(t.y >> 5) & (kHotRowWords - 1u)] >> (t.y & 31u)) & 1u) {
-        // a row with hot tiles: is this one of them?  lane j tests the row's slot o0 + j, o0 + j + 64, ...
-        const uint32_t me = (t.y << 12) | t.x, lane = threadIdx.x & 63u;
-        const uint32_t o0 = kp.hot[kMaxHotTiles + t.y], o1 = kp.hot[kMaxHotTiles + t.y + 1u];
-        bool dup = false;
-        for (uint32_t i = o0; i < o1; i += 64u)
-            if (i + lane < o1 && (kp.hot[i + lane] >> 4) == me) dup = true;
-        t.run = __ballot(dup) == 0ull;
     }
     return t;
-}
-
-__device__ __forceinline__ TileSplit tile_split(const KParams& kp, const LaunchTile& t) {
-    TileSplit s{t.part, t.parts, nullptr, nullptr, false};
-    if (t.parts > 1u) {
-        const size_t g = (size_t)t.slot * kp.nframes + t.z;
-        s.terms = kp.xterms + g * kp.num_lights * 3u * 64u;
-        s.count = kp.xcount + g;
-    }
-    return s;
 }
 
 // One lane per pixel; wave = workgroup = 8x8 tile (RRTE_WG256: 16x16-pixel workgroups).  Every lane
@@ -2078,7 +1991,6 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK
     const uint32_t nsamples = SINGLE ? 1u : kp.spp;
     const uint32_t pmask = camera_tile_mask(kp, cm, tile.x, tile.y);
-    TileSplit sp = tile_split(kp, tile);
     // camera ray of sample s (raytracer.rs:66-70): per-(pixel, sample) RNG stream, jitter, generate_ray
     auto camera_ray = [&](uint32_t s, uint32_t& st) {
         st = pcg_hash(pcg_hash(pcg_hash(kp.seed) ^ pix) ^ s);
@@ -2130,21 +2042,21 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
             Ray r = camera_ray(s, st);
             Col c{0.0f, 0.0f, 0.0f, 1.0f};
             if (MODE == RRTE_MODE_LAMBERT_SHADOW) {
-                c = shade_lambert<S, CULL>(sc, kp, cl, r, live, nshadow, pmask, sp);
+                c = shade_lambert<S, CULL>(sc, kp, cl, r, live, nshadow, pmask);
             } else if (live) {
                 c = ray_color_ref<S, SINGLE>(sc, kp, r, st, SINGLE ? pmask : ~0u);
             }
             accumulate(c);
         }
     }
-    if (live && !sp.skip_store) {  // (a split tile's pixels are written by its last part)
+    if (live) {
         acc.r = acc.r * kp.inv_spp;
         acc.g = acc.g * kp.inv_spp;
         acc.b = acc.b * kp.inv_spp;
         acc.a = acc.a * kp.inv_spp;
         const float ig = kp.inv_gamma;
         const float ga = rclamp(acc.a);
-        const size_t o = (size_t)lr * kp.width + x;  // packed local rows
+        const size_t o = (size_t)(kp.out_image_rows ? y : lr) * kp.width + x;  // packed local rows, or image rows
         // the parity float buffer (or a gamma other than the reference's 2.2) needs powf itself
         const bool exact_pow = (out_f32 && !stamps) || ig != kInvGamma22;
         float gr = 0.0f, gg = 0.0f, gb = 0.0f;
@@ -2189,11 +2101,11 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
             atomicAdd(counters + shard * kCounterStride, (unsigned long long)v);
         }
     }
-    if (kWg64 && kp.tile_cost && tile.z == 0u && lane == 0)  // tile profile (TileProfile, rrte_hip.hip); a split
-        atomicMax(kp.tile_cost + brow * tiles_x + tile.x, (uint32_t)(wall_clock64() - t_wave0));  // tile: its slowest part
+    if (kWg64 && kp.tile_cost && tile.z == 0u && lane == 0)  // tile profile (TileProfile, rrte_hip.hip)
+        kp.tile_cost[brow * tiles_x + tile.x] = (uint32_t)(wall_clock64() - t_wave0);
     if (stamps && lane == 0) {
         const uint64_t t1 = wall_clock64();
-        const uint32_t wid = (brow * tiles_x + tile.x) * 4u + (kWg64 ? tile.part : wave);  // split parts: own slot
+        const uint32_t wid = (brow * tiles_x + tile.x) * 4u + wave;
         uint32_t* s = reinterpret_cast<uint32_t*>(out_f32) + 4u * wid;
         s[0] = (uint32_t)t_wave0;
         s[1] = (uint32_t)(t_wave0 >> 32);

@@ -43,21 +43,31 @@ struct LaunchPlan {
     bool cull, single;
     uint32_t num_prims, num_lights, num_materials;
     uint32_t gx, gy;
-    uint32_t cold_rows = 0;  // image-order workgroup rows after the hot rows (gy, or 0 for an LPT list)
 };
 
-constexpr double kSplitFracDefault = 0.7;  // see compose_slots
-
-// A tile order composed off the render thread (plan_tile_order): the profile's shape key, the measured
-// tiles in dispatch priority and the slot list for `parts` parts per split tile.
+// A tile order composed off the render thread (plan_tile_order): the profile's shape key and the
+// slot list (every tile, slowest first).
 struct TilePlanResult {
     std::string key;
-    std::vector<std::pair<uint32_t, uint32_t>> top;
-    uint32_t top_max = 0;
     std::vector<uint32_t> slots;
-    uint32_t row_bits[kHotRowWords] = {};
-    bool has_split = false;
-    uint32_t parts = 0;
+};
+
+// A device resource that launches read asynchronously (a scene version, a tile-list version): the
+// streams that launched work reading it since it became current, and -- once it is retired -- one
+// event per such stream recorded at retirement, after that stream's last launch that read it.  The
+// resource may be overwritten or freed once every event has completed.  No event is recorded per
+// launch (an event after every launch put a gap between one stream's launches).
+// Streams handed to the async entry points must therefore stay valid until the context has been
+// synchronised (include/rrte_hip.h).
+struct Retire {
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> events;
+    size_t nev = 0;
+    void use(hipStream_t st) {
+        for (hipStream_t s : streams)
+            if (s == st) return;
+        streams.push_back(st);
+    }
 };
 
 struct rrte_ctx {
@@ -65,19 +75,38 @@ struct rrte_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     std::string err;
-    // scene cache (device copy + the host bytes it was made from)
+    // scene cache (device copy + the host bytes it was made from).  The device copy is versioned: a
+    // ring of kSceneVersions buffer sets, so a scene change uploads into a version no frame in flight
+    // reads (Retire) instead of draining the device; d_prims ... mesh_view alias the current version.
     std::vector<unsigned char> scene_key;
-    DPrim* d_prims = nullptr; size_t cap_prims = 0;
-    DMaterial* d_mats = nullptr; size_t cap_mats = 0;
-    DLight* d_lights = nullptr; size_t cap_lights = 0;
-    rrte_sdf_node* d_nodes = nullptr; size_t cap_nodes = 0;
-    float4* d_bounds = nullptr; size_t cap_bounds = 0;  // culling spheres, one per object
-    // triangle meshes: BVH nodes, triangle slots, normals, original-order permutation (bvh.hip)
-    float4* d_mesh_nodes = nullptr; size_t cap_mesh_nodes = 0;
-    float4* d_mesh_tris = nullptr; size_t cap_mesh_tris = 0;
-    float4* d_mesh_norms = nullptr; size_t cap_mesh_norms = 0;
-    uint32_t* d_mesh_perm = nullptr; size_t cap_mesh_perm = 0;
+    struct SceneBuf {
+        DPrim* d_prims = nullptr; size_t cap_prims = 0;
+        DMaterial* d_mats = nullptr; size_t cap_mats = 0;
+        DLight* d_lights = nullptr; size_t cap_lights = 0;
+        rrte_sdf_node* d_nodes = nullptr; size_t cap_nodes = 0;
+        float4* d_bounds = nullptr; size_t cap_bounds = 0;  // culling spheres, one per object
+        // triangle meshes: BVH nodes, triangle slots, normals, original-order permutation (bvh.hip)
+        float4* d_mesh_nodes = nullptr; size_t cap_mesh_nodes = 0;
+        float4* d_mesh_tris = nullptr; size_t cap_mesh_tris = 0;
+        float4* d_mesh_norms = nullptr; size_t cap_mesh_norms = 0;
+        uint32_t* d_mesh_perm = nullptr; size_t cap_mesh_perm = 0;
+        Retire ret;
+    };
+    static constexpr int kSceneVersions = 4;
+    SceneBuf sb[kSceneVersions];
+    int sb_cur = -1;
+    hipStream_t upload_stream = nullptr;  // scene H2D copies (never queued behind frames or gathers)
+    DPrim* d_prims = nullptr;
+    DMaterial* d_mats = nullptr;
+    DLight* d_lights = nullptr;
+    rrte_sdf_node* d_nodes = nullptr;
+    float4* d_bounds = nullptr;
     MeshView mesh_view{};
+    // device buffers replaced by larger ones while launches in flight may still read them: freed at
+    // the next point where the context is idle (rrte_hip_synchronize, rrte_hip_destroy) instead of by a
+    // hipFree that could wait on the device
+    std::vector<void*> graveyard;
+    Retire launched;                 // every stream that launched a frame since the last synchronisation
     uint32_t n_prims = 0, n_mats = 0, n_lights = 0, n_nodes = 0;
     // frame buffers for the blocking entry points
     uint32_t* d_rgba = nullptr; size_t cap_rgba = 0;
@@ -199,59 +228,39 @@ struct rrte_ctx {
     // order).  The order never changes a pixel, only when each tile starts.  RRTE_TILE_ORDER=0 turns it
     // off (A/B, tests).
     struct TileProfile {
-        std::string key;                 // launch shape the hot list belongs to
+        std::string key;                 // launch shape the tile list belongs to
         std::string pending_key;         // shape of the profile in flight
         bool pending = false;
         hipEvent_t ev = nullptr;         // the profile's D2H copy done
         uint32_t* d_cost = nullptr; size_t cap_d = 0;
         uint32_t* h_cost = nullptr; size_t cap_h = 0;  // pinned
         uint32_t tiles = 0, tiles_x = 0;                 // of the pending profile
-        // the measured slowest tiles, slowest first (tile index, 100 MHz ticks), and the slot list
-        // composed from them for `slots_parts` parts per split tile (at most kMaxHotTiles slots)
-        std::vector<std::pair<uint32_t, uint32_t>> top;
-        uint32_t top_max = 0;
         bool fixed = false;              // RRTE_TILE_ORDER=2 list
-        std::vector<uint32_t> slots;     // packed hot_pack slots, ascending
-        uint32_t slots_parts = 0;
-        // device copies of slot lists (KParams::hot): a pool of immutable versions, one per upload; when
-        // the pool is used up the device is synchronised once and every version is free again (no
-        // per-launch bookkeeping: an event recorded after each launch put a gap between the launches
-        // of one stream)
+        std::vector<uint32_t> slots;     // packed hot_pack slots in dispatch order (every tile once)
+        // device copies of slot lists (KParams::hot): a pool of immutable versions, one per upload.  The
+        // current version is retired (Retire) when the next one is uploaded; an upload takes a retired
+        // version whose launches have all completed, and when none has, the launch keeps the current
+        // list (a stale order renders the same pixels) -- no render call ever waits for one.
         static constexpr int kVersions = 16;
         uint32_t* d_list[kVersions] = {};
         size_t cap_list[kVersions] = {};  // words
+        Retire ret[kVersions];
         uint32_t* h_list = nullptr;      // pinned staging
         size_t cap_h_list = 0;
-        bool lpt = false;                // RRTE_TILE_ORDER=3: every tile in measured-cost order
-        bool has_split = false;          // some slot of `slots` is a split part
         hipStream_t upload_stream = nullptr;
         int cur = -1;                    // version holding `slots` (-1: not uploaded)
-        int next_version = 0;
-        uint32_t row_bits[kHotRowWords] = {};
         uint64_t launches = 0;           // launches of `key` since its last profile
         uint64_t profiles = 0;           // completed profiles
+        uint64_t uploads = 0;            // list versions uploaded
         uint64_t cam_sig = 0;            // camera of the last profiled launch (frame 0's FrameCam)
         std::future<TilePlanResult> work;  // composition of the last profile's order (worker thread)
         bool working = false;
     } tprof;
-    // Exchange areas of split tiles (KParams::xterms / xcount), one per launch in a ring; an area is
-    // reused after the launch that last used it has completed (else the new launch waits for it)
-    struct XArea {
-        float* terms = nullptr; size_t cap_terms = 0;
-        uint32_t* count = nullptr; size_t cap_count = 0;  // zero between uses (the last part resets)
-        hipEvent_t ev = nullptr;
-        bool used = false;
-    };
-    static constexpr int kXAreas = 8;
-    XArea xarea[kXAreas];
-    int xnext = 0;
-    bool env_tile_split = false;       // RRTE_TILE_SPLIT=1: split the slowest hot tiles (measured slower)
-    double split_frac = kSplitFracDefault;  // RRTE_SPLIT_FRAC
-    bool env_split_noevent = false;    // RRTE_SPLIT_NOEVENT=1 (timing only): exchange areas reused without events
     bool env_tile_order = true;
-    bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed spread-out hot list (tests)
-    bool env_tile_order_lpt = true;     // every tile in measured-cost order (default; RRTE_TILE_ORDER=1: the
-                                        // 1024 slowest first, then image order)
+    bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed scrambled permutation of the tiles (tests)
+    // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
+    // per launch, so the version pool wraps within a few frames)
+    bool env_test_recycle = false;
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
     struct {
         bool valid = false;
@@ -266,6 +275,8 @@ struct rrte_ctx {
 static rrte_status flush_batch(rrte_ctx* c);
 static rrte_status render_batch(rrte_ctx* c, bool at_flush);
 static rrte_status wait_bounded(rrte_ctx* c);
+static rrte_status poll_events(rrte_ctx* c, const hipEvent_t* ev, size_t n);
+static rrte_status nccl_settle(rrte_ctx* c, ncclResult_t r, const char* what);
 
 namespace {
 
@@ -305,23 +316,74 @@ rrte_status fail(rrte_ctx* c, rrte_status st, const char* fmt, ...) {
             return fail((ctx), RRTE_HIP_ERROR, "%s failed: %s", #expr, hipGetErrorString(e_));     \
     } while (0)
 
+// (the communicator is non-blocking: ncclInProgress is settled by polling, nccl_settle)
 #define NCCLCHK(ctx, expr)                                                                         \
     do {                                                                                           \
         ncclResult_t r_ = (expr);                                                                  \
-        if (r_ != ncclSuccess)                                                                     \
-            return fail((ctx), RRTE_RCCL_ERROR, "%s failed: %s", #expr, ncclGetErrorString(r_));   \
+        if (r_ != ncclSuccess) {                                                                   \
+            rrte_status s_ = nccl_settle((ctx), r_, #expr);                                        \
+            if (s_ != RRTE_OK) return s_;                                                          \
+        }                                                                                          \
     } while (0)
 
+// Device buffer of at least n elements; a smaller one goes to the graveyard (launches in flight may
+// still read it; freed when the context is next idle).
 template <typename T>
 rrte_status ensure(rrte_ctx* c, T*& ptr, size_t& cap, size_t n) {
     if (n <= cap && ptr) return RRTE_OK;
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) c->graveyard.push_back(ptr);
     ptr = nullptr;
     cap = 0;
     size_t want = n < 1 ? 1 : n;
     HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&ptr), want * sizeof(T)));
     cap = want;
     return RRTE_OK;
+}
+
+// Retire a resource (struct Retire): an event on every stream that read it since it became current.
+// Events of an earlier retirement that have not completed yet are kept.
+rrte_status retire(rrte_ctx* c, Retire& r) {
+    size_t keep = 0;
+    for (size_t i = 0; i < r.nev; ++i)
+        if (hipEventQuery(r.events[i]) != hipSuccess) std::swap(r.events[keep++], r.events[i]);
+    r.nev = keep;
+    for (hipStream_t s : r.streams) {
+        if (r.events.size() <= r.nev) {
+            hipEvent_t e = nullptr;
+            HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            r.events.push_back(e);
+        }
+        HIPCHK(c, hipEventRecord(r.events[r.nev], s));
+        ++r.nev;
+    }
+    r.streams.clear();
+    return RRTE_OK;
+}
+
+// True when every launch that read a retired resource has completed (no wait).
+bool retired_done(const Retire& r) {
+    for (size_t i = 0; i < r.nev; ++i)
+        if (hipEventQuery(r.events[i]) != hipSuccess) return false;
+    return true;
+}
+
+// Bounded wait for a retired resource (poll_events: RRTE_RCCL_ERROR if a gather it sits behind stalls).
+rrte_status wait_retired(rrte_ctx* c, Retire& r) {
+    if (retired_done(r)) {
+        r.nev = 0;
+        return RRTE_OK;
+    }
+    rrte_status st = poll_events(c, r.events.data(), r.nev);
+    if (st == RRTE_OK) r.nev = 0;
+    return st;
+}
+
+void destroy_events(Retire& r) {
+    for (hipEvent_t e : r.events)
+        if (e) (void)hipEventDestroy(e);
+    r.events.clear();
+    r.nev = 0;
+    r.streams.clear();
 }
 
 // ---- glam restatement on the host (same algorithms as oracle/, see there) ----
@@ -654,14 +716,11 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         ++c->same_scene_renders;
         return RRTE_OK;
     }
-    c->same_scene_renders = 0;
-    ++c->scene_gen;
+    (void)st;  // the copies run on the context's upload stream, complete before any launch is enqueued
 
     for (uint32_t k = 0; k < s->num_mesh_indices; ++k)
         if (s->mesh_indices[k] >= s->num_mesh_vertices)
             return fail(c, RRTE_INVALID_ARG, "mesh index %u out of range (%u vertices)", k, s->num_mesh_vertices);
-    // frames still in flight (possibly on other streams) read the current scene buffers
-    HIPCHK(c, hipDeviceSynchronize());
     std::vector<DPrim> prims;
     std::vector<DMaterial> mats;
     std::vector<DLight> lights;
@@ -670,42 +729,63 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     MeshData md;
     build_mesh_bvhs(s, prims.data(), md, bounds.data());
     if (md.too_deep) return fail(c, RRTE_UNSUPPORTED_PRIM, "mesh BVH deeper than the traversal stack");
-    rrte_status r;
-    if ((r = ensure(c, c->d_prims, c->cap_prims, prims.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, c->d_bounds, c->cap_bounds, bounds.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, c->d_mats, c->cap_mats, mats.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, c->d_lights, c->cap_lights, lights.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, c->d_nodes, c->cap_nodes, (size_t)s->num_sdf_nodes)) != RRTE_OK) return r;
-    if ((r = ensure(c, c->d_mesh_nodes, c->cap_mesh_nodes, md.nodes.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, c->d_mesh_tris, c->cap_mesh_tris, md.tris.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, c->d_mesh_norms, c->cap_mesh_norms, md.norms.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, c->d_mesh_perm, c->cap_mesh_perm, md.perm.size())) != RRTE_OK) return r;
-    HIPCHK(c, hipEventRecord(c->ev2, st));
-    auto put = [&](void* dst, const void* src, size_t bytes) -> rrte_status {
-        if (bytes) HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
-        return RRTE_OK;
-    };
-    if ((r = put(c->d_prims, prims.data(), prims.size() * sizeof(DPrim))) != RRTE_OK) return r;
-    if ((r = put(c->d_mats, mats.data(), mats.size() * sizeof(DMaterial))) != RRTE_OK) return r;
-    if ((r = put(c->d_lights, lights.data(), lights.size() * sizeof(DLight))) != RRTE_OK) return r;
     // SDF programs with their exact CSG early-outs (sdf_guard.hpp); the key above stays the caller's IR
     std::vector<rrte_sdf_node> nodes = decorate_scene_sdf(s, c->env_guard_leaves);
     JitTopo topo;
     std::string tkey = topology_of(prims, lights, nodes, topo);
-    if ((r = put(c->d_nodes, nodes.data(), bn)) != RRTE_OK) return r;
-    if ((r = put(c->d_bounds, bounds.data(), bounds.size() * sizeof(float4))) != RRTE_OK) return r;
-    if ((r = put(c->d_mesh_nodes, md.nodes.data(), md.nodes.size() * sizeof(float4))) != RRTE_OK) return r;
-    if ((r = put(c->d_mesh_tris, md.tris.data(), md.tris.size() * sizeof(float4))) != RRTE_OK) return r;
-    if ((r = put(c->d_mesh_norms, md.norms.data(), md.norms.size() * sizeof(float4))) != RRTE_OK) return r;
-    if ((r = put(c->d_mesh_perm, md.perm.data(), md.perm.size() * sizeof(uint32_t))) != RRTE_OK) return r;
-    // the staging vectors die at return: make the copies complete first
-    HIPCHK(c, hipStreamSynchronize(st));
-    HIPCHK(c, hipEventRecord(c->ev0, st));
-    HIPCHK(c, hipEventSynchronize(c->ev0));
+
+    // Frames in flight keep reading the current version: retire it and upload into the next version
+    // of the ring once the frames that read THAT one have completed (normally long ago: a wait here
+    // means more scene changes than versions within the frames in flight; bounded, like every wait
+    // that may sit behind a gather)
+    rrte_status r;
+    if (c->sb_cur >= 0 && (r = retire(c, c->sb[c->sb_cur].ret)) != RRTE_OK) return r;
+    const int nx = (c->sb_cur + 1) % rrte_ctx::kSceneVersions;
+    rrte_ctx::SceneBuf& B = c->sb[nx];
+    if ((r = wait_retired(c, B.ret)) != RRTE_OK) return r;
+    c->same_scene_renders = 0;
+    ++c->scene_gen;
+    c->sb_cur = -1;  // (until the upload has completed: a failure below leaves no current version)
+    c->scene_key.clear();
+    if ((r = ensure(c, B.d_prims, B.cap_prims, prims.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, B.d_bounds, B.cap_bounds, bounds.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, B.d_mats, B.cap_mats, mats.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, B.d_lights, B.cap_lights, lights.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, B.d_nodes, B.cap_nodes, (size_t)s->num_sdf_nodes)) != RRTE_OK) return r;
+    if ((r = ensure(c, B.d_mesh_nodes, B.cap_mesh_nodes, md.nodes.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, B.d_mesh_tris, B.cap_mesh_tris, md.tris.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, B.d_mesh_norms, B.cap_mesh_norms, md.norms.size())) != RRTE_OK) return r;
+    if ((r = ensure(c, B.d_mesh_perm, B.cap_mesh_perm, md.perm.size())) != RRTE_OK) return r;
+    if (!c->upload_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking));
+    hipStream_t us = c->upload_stream;
+    HIPCHK(c, hipEventRecord(c->ev2, us));
+    auto put = [&](void* dst, const void* src, size_t bytes) -> rrte_status {
+        if (bytes) HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, us));
+        return RRTE_OK;
+    };
+    if ((r = put(B.d_prims, prims.data(), prims.size() * sizeof(DPrim))) != RRTE_OK) return r;
+    if ((r = put(B.d_mats, mats.data(), mats.size() * sizeof(DMaterial))) != RRTE_OK) return r;
+    if ((r = put(B.d_lights, lights.data(), lights.size() * sizeof(DLight))) != RRTE_OK) return r;
+    if ((r = put(B.d_nodes, nodes.data(), bn)) != RRTE_OK) return r;
+    if ((r = put(B.d_bounds, bounds.data(), bounds.size() * sizeof(float4))) != RRTE_OK) return r;
+    if ((r = put(B.d_mesh_nodes, md.nodes.data(), md.nodes.size() * sizeof(float4))) != RRTE_OK) return r;
+    if ((r = put(B.d_mesh_tris, md.tris.data(), md.tris.size() * sizeof(float4))) != RRTE_OK) return r;
+    if ((r = put(B.d_mesh_norms, md.norms.data(), md.norms.size() * sizeof(float4))) != RRTE_OK) return r;
+    if ((r = put(B.d_mesh_perm, md.perm.data(), md.perm.size() * sizeof(uint32_t))) != RRTE_OK) return r;
+    HIPCHK(c, hipEventRecord(c->ev0, us));
+    // the staging vectors die at return, and launches enqueued after this call must see the bytes: the
+    // upload stream holds nothing but these copies, so this wait is bounded by the transfer
+    HIPCHK(c, hipStreamSynchronize(us));
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, c->ev2, c->ev0);
     *upload_ms = ms;
-    c->mesh_view = MeshView{c->d_mesh_nodes, c->d_mesh_tris, c->d_mesh_norms, c->d_mesh_perm};
+    c->sb_cur = nx;
+    c->d_prims = B.d_prims;
+    c->d_mats = B.d_mats;
+    c->d_lights = B.d_lights;
+    c->d_nodes = B.d_nodes;
+    c->d_bounds = B.d_bounds;
+    c->mesh_view = MeshView{B.d_mesh_nodes, B.d_mesh_tris, B.d_mesh_norms, B.d_mesh_perm};
     c->h_prims = prims;
     c->h_bounds = bounds;
     c->h_mats = mats;
@@ -960,7 +1040,10 @@ JitKernel* jit_lookup(rrte_ctx* c, const std::string& key, bool topo, int mode, 
         if (c->jit_cache.size() >= 32) {
             // frames launched from these modules may still run on caller streams (a mode / cull /
             // sample-count change does not re-upload the scene, so upload_scene's sync has not run)
-            if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+            // (bounded: RRTE_RCCL_ERROR surfaces at the next gather call if a stalled gather blocks it)
+            if (hipSetDevice(c->device) != hipSuccess || retire(c, c->launched) != RRTE_OK ||
+                wait_retired(c, c->launched) != RRTE_OK)
+                return nullptr;
             for (auto& kv : c->jit_cache) jit_release(kv.second);
             c->jit_cache.clear();
             c->jit_last.valid = false;
@@ -1037,7 +1120,7 @@ LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_pa
     return L;
 }
 
-// Hot-first tile order (rrte_ctx::TileProfile, KParams::hot).
+// Measured-cost tile order (rrte_ctx::TileProfile, KParams::hot).
 constexpr uint64_t kTileReprofile = 256;  // launches of one shape between two profiles (each costs a list upload)
 constexpr uint64_t kTileReprofileMoving = 32;  // ... when the camera has moved since the last profile
 
@@ -1047,112 +1130,42 @@ uint64_t fnv1a(const void* p, size_t n) {
     return h;
 }
 
-// The slowest tiles of a completed profile: at most kMaxHotTiles, each at least twice the mean tile
-// time and a quarter of the slowest, slowest first.
-void build_hot_list(rrte_ctx::TileProfile& tp) {
-    const uint32_t n = tp.tiles;
-    tp.top.clear();
-    tp.slots.clear();
-    tp.slots_parts = 0;
-    tp.fixed = false;
-    if (n == 0 || tp.tiles_x == 0) return;
-    double sum = 0.0;
+// Every tile of a profile (costs[0 .. n), tiles_x per row), slowest first (longest-processing-time
+// order), as packed slots: a counting sort on 65536 cost buckets (ties in tile order), O(tiles) on the
+// host.
+std::vector<uint32_t> lpt_slots(const uint32_t* costs, uint32_t n, uint32_t tiles_x) {
+    std::vector<uint32_t> slots;
+    if (n == 0 || tiles_x == 0) return slots;
     uint32_t mx = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        sum += tp.h_cost[i];
-        mx = std::max(mx, tp.h_cost[i]);
+    for (uint32_t i = 0; i < n; ++i) mx = std::max(mx, costs[i]);
+    constexpr uint32_t B = 65536;
+    std::vector<uint32_t> cnt(B + 1, 0u);
+    auto bucket = [&](uint32_t c) { return B - 1 - (mx ? (uint32_t)((uint64_t)c * (B - 1) / mx) : 0u); };
+    for (uint32_t i = 0; i < n; ++i) ++cnt[bucket(costs[i])];
+    uint32_t acc = 0;
+    for (uint32_t b = 0; b <= B; ++b) {
+        const uint32_t c = cnt[b];
+        cnt[b] = acc;
+        acc += c;
     }
-    tp.top_max = mx;
-    if (tp.lpt) {
-        // RRTE_TILE_ORDER=3: every tile, slowest first (longest-processing-time order), by a counting
-        // sort on 65536 cost buckets (ties in tile order): O(tiles) on the host
-        constexpr uint32_t B = 65536;
-        std::vector<uint32_t> cnt(B + 1, 0u);
-        auto bucket = [&](uint32_t c) { return mx ? (uint32_t)((uint64_t)c * (B - 1) / mx) : 0u; };
-        for (uint32_t i = 0; i < n; ++i) ++cnt[B - 1 - bucket(tp.h_cost[i])];
-        uint32_t acc = 0;
-        for (uint32_t b = 0; b <= B; ++b) {
-            const uint32_t c = cnt[b];
-            cnt[b] = acc;
-            acc += c;
-        }
-        tp.top.resize(n);
-        for (uint32_t i = 0; i < n; ++i) tp.top[cnt[B - 1 - bucket(tp.h_cost[i])]++] = {i, tp.h_cost[i]};
-        return;
-    }
-    // the candidates above the threshold first (a few percent of the tiles), then a sort of those
-    // only: this runs on the host inside a render call (a partial sort over every tile took ~0.7 ms)
-    const double thr = std::max(2.0 * sum / n, 0.25 * mx);
-    const uint32_t t = (uint32_t)std::min<double>(std::ceil(thr), 4294967295.0);
-    for (uint32_t i = 0; i < n; ++i)
-        if (tp.h_cost[i] >= t) tp.top.emplace_back(i, tp.h_cost[i]);
-    auto slower = [](const std::pair<uint32_t, uint32_t>& a, const std::pair<uint32_t, uint32_t>& b) {
-        return a.second > b.second || (a.second == b.second && a.first < b.first);
-    };
-    if (tp.top.size() > kMaxHotTiles) {
-        std::nth_element(tp.top.begin(), tp.top.begin() + kMaxHotTiles, tp.top.end(), slower);
-        tp.top.resize(kMaxHotTiles);
-    }
-    std::sort(tp.top.begin(), tp.top.end(), slower);
+    slots.resize(n);
+    for (uint32_t i = 0; i < n; ++i) slots[cnt[bucket(costs[i])]++] = hot_pack(i % tiles_x, i / tiles_x);
+    return slots;
 }
 
-// Split tiles: a hot tile at least this fraction of the slowest one (RRTE_SPLIT_FRAC, default 0.7) is
-// rendered as one part per shadow-casting light (at most 4), so its lights' shadow marches run on
-// different waves at once; every part repeats the tile's camera rays, so only the tail tiles pay.
-
-// Hot slots for `parts` parts per split tile (1: no splitting), ascending.
-void compose_slots(rrte_ctx::TileProfile& tp, uint32_t parts, uint32_t tiles_x, uint32_t tiles, double split_frac) {
-    tp.slots.clear();
-    memset(tp.row_bits, 0, sizeof tp.row_bits);
-    tp.slots_parts = parts;
-    tp.cur = -1;
-    tp.has_split = false;
-    auto add = [&](uint32_t i, uint32_t np) {
-        const uint32_t x = i % tiles_x, y = i / tiles_x;
-        tp.has_split |= np > 1;
-        for (uint32_t q = 0; q < np; ++q) tp.slots.push_back(hot_pack(x, y, q, np));
-        tp.row_bits[y >> 5] |= 1u << (y & 31u);
-    };
-    if (tp.fixed) {
-        // RRTE_TILE_ORDER=2 (tests): tiles spread over the frame, first and last included, every other
-        // one split when splitting is possible; as many as fit in kMaxHotTiles slots
-        uint32_t m = std::min<uint32_t>(tiles, kMaxHotTiles);
-        while (m > 1 && (m + 1) / 2 * parts + m / 2 > kMaxHotTiles) --m;
-        for (uint32_t j = 0; j < m; ++j) add(m > 1 ? (uint32_t)((uint64_t)j * (tiles - 1) / (m - 1)) : 0u, j % 2 ? 1u : parts);
-    } else if (tp.lpt) {
-        // every tile in cost order; the split ones come first (they are the slowest), and their slots
-        // stay below kMaxHotTiles (the split exchange areas are sized for that many slots)
-        for (const auto& t : tp.top) {
-            uint32_t np = parts > 1 && t.second >= split_frac * tp.top_max ? parts : 1u;
-            if (np > 1 && tp.slots.size() + np > kMaxHotTiles) np = 1u;
-            add(t.first, np);
-        }
-        memset(tp.row_bits, 0, sizeof tp.row_bits);  // no image-order rows follow
-        return;
-    } else {
-        for (const auto& t : tp.top) {
-            const uint32_t np = parts > 1 && t.second >= split_frac * tp.top_max ? parts : 1u;
-            if (tp.slots.size() + np > kMaxHotTiles) break;
-            add(t.first, np);
-        }
+// RRTE_TILE_ORDER=2 (tests): every tile once in a fixed scrambled order -- slot k takes tile
+// (k * stride) mod n for a stride near 0.618 n coprime with n -- so the list path runs on every launch
+// without a profile.
+std::vector<uint32_t> fixed_slots(uint32_t n, uint32_t tiles_x) {
+    std::vector<uint32_t> slots(n);
+    uint64_t stride = std::max<uint64_t>(1, (uint64_t)(0.618034 * n));
+    auto gcd = [](uint64_t a, uint64_t b) { while (b) { const uint64_t t = a % b; a = b; b = t; } return a; };
+    while (n > 1 && gcd(stride, n) != 1) ++stride;
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t i = (uint32_t)((k * stride) % n);
+        slots[k] = hot_pack(i % tiles_x, i / tiles_x);
     }
-    std::sort(tp.slots.begin(), tp.slots.end());
-}
-
-// Parts of a split tile for this launch (1: no splitting): LAMBERT_SHADOW frames of one sample whose
-// scene has at least two shadow-casting lights (one part each, at most 4; ambient lights go to part 0).
-uint32_t split_parts(const rrte_ctx* c, const LaunchPlan& L, uint32_t light_part[kMaxSplitLights / 16]) {
-    memset(light_part, 0, sizeof(uint32_t) * (kMaxSplitLights / 16));
-    if (!c->env_tile_split || L.mode != RRTE_MODE_LAMBERT_SHADOW || L.k.spp != 1 || L.k.max_depth == 0 ||
-        L.num_lights > kMaxSplitLights || c->h_lights.size() < L.num_lights)
-        return 1;
-    uint32_t casters = 0;
-    for (uint32_t i = 0; i < L.num_lights; ++i) casters += c->h_lights[i].kind != RRTE_LIGHT_AMBIENT;
-    const uint32_t parts = std::min<uint32_t>(casters, 4u);
-    if (parts < 2) return 1;
-    for (uint32_t i = 0, q = 0; i < L.num_lights; ++i)
-        if (c->h_lights[i].kind != RRTE_LIGHT_AMBIENT) light_part[i >> 4] |= ((q++ % parts) & 3u) << ((i & 15u) * 2u);
-    return parts;
+    return slots;
 }
 
 // Allocates what an upload of up to `words` list words needs -- pinned staging, the upload stream and
@@ -1161,7 +1174,7 @@ uint32_t split_parts(const rrte_ctx* c, const LaunchPlan& L, uint32_t light_part
 bool reserve_hot_lists(rrte_ctx* c, size_t words) {
     auto& tp = c->tprof;
     if (tp.cap_h_list < words) {
-        if (tp.h_list) (void)hipHostFree(tp.h_list);
+        if (tp.h_list) (void)hipHostFree(tp.h_list);  // (pinned staging: every copy from it was synchronised)
         tp.h_list = nullptr;
         tp.cap_h_list = 0;
         if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), words * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
@@ -1177,104 +1190,67 @@ bool reserve_hot_lists(rrte_ctx* c, size_t words) {
     return true;
 }
 
-// Uploads the composed slots and their tile-row offsets into the next version of the device list
-// (kHotListWords words); false leaves the launch in image order.  The copy completes before any later
-// launch is enqueued (its own stream, synchronised), so every launch sees a whole list.
-bool upload_hot_list(rrte_ctx* c, uint32_t tiles_y) {
+// Uploads the composed slots into a free version of the device list; false leaves the launch on the
+// current list (or in image order) -- it never waits for the device.  The current version is retired
+// first; a version is free once every launch that read it has completed (struct Retire).  The copy
+// runs on the list's own upload stream and is synchronised (it holds nothing else), so every launch
+// sees a whole list.
+bool upload_hot_list(rrte_ctx* c) {
     auto& tp = c->tprof;
-    if (tp.next_version == rrte_ctx::TileProfile::kVersions) {
-        // every version may still be read by a launch in flight: wait for all of them, once per
-        // kVersions uploads (one upload per profile, i.e. per kTileReprofile launches at most)
-        if (hipDeviceSynchronize() != hipSuccess) return false;
-        tp.next_version = 0;
+    constexpr int K = rrte_ctx::TileProfile::kVersions;
+    int pick = -1;
+    for (int k = 1; k <= K && pick < 0; ++k) {  // the oldest retired version first
+        const int v = (int)((tp.uploads + (uint64_t)k) % K);
+        if (v != tp.cur && retired_done(tp.ret[v])) pick = v;
     }
-    const int pick = tp.next_version++;
-    // kHotListWords (slots + row offsets) or, for a whole-frame LPT list, one word per slot
-    const size_t words = std::max<size_t>(kHotListWords, tp.slots.size());
+    if (pick < 0) return false;
+    tp.ret[pick].nev = 0;
+    const size_t words = tp.slots.size();
     const size_t bytes = words * sizeof(uint32_t);
-    if (tp.cap_list[pick] < words) {
-        // a version that may still be read is only ever replaced after the pool's device sync above,
-        // so a larger one for a larger frame needs a sync of its own (rare: a new frame size)
-        if (tp.d_list[pick] && (hipDeviceSynchronize() != hipSuccess || hipFree(tp.d_list[pick]) != hipSuccess)) return false;
+    if (tp.cap_list[pick] < words) {  // a larger frame: its launches have completed, the old buffer is idle
+        if (tp.d_list[pick]) c->graveyard.push_back(tp.d_list[pick]);
         tp.d_list[pick] = nullptr;
         tp.cap_list[pick] = 0;
         if (hipMalloc(reinterpret_cast<void**>(&tp.d_list[pick]), bytes) != hipSuccess) return false;
         tp.cap_list[pick] = words;
     }
-    if (tp.cap_h_list < words) {
-        if (tp.h_list) (void)hipHostFree(tp.h_list);
-        tp.h_list = nullptr;
-        tp.cap_h_list = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), bytes, hipHostMallocDefault) != hipSuccess) return false;
-        tp.cap_h_list = words;
-    }
-    memset(tp.h_list, 0, bytes);
-    memcpy(tp.h_list, tp.slots.data(), tp.slots.size() * sizeof(uint32_t));
-    if (!tp.lpt) {
-        uint32_t* off = tp.h_list + kMaxHotTiles;
-        for (uint32_t y = 0, i = 0; y <= std::min<uint32_t>(tiles_y, kHotRows); ++y) {
-            while (i < tp.slots.size() && hot_y(tp.slots[i]) < y) ++i;
-            off[y] = i;
-        }
-    }
-    // a stream of its own: the context's stream may hold a blocking entry point's gather
-    if (!tp.upload_stream && hipStreamCreateWithFlags(&tp.upload_stream, hipStreamNonBlocking) != hipSuccess) return false;
+    if (!reserve_hot_lists(c, words)) return false;
+    memcpy(tp.h_list, tp.slots.data(), bytes);
     if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
         hipStreamSynchronize(tp.upload_stream) != hipSuccess)
         return false;
+    if (tp.cur >= 0 && retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
     tp.cur = pick;
+    ++tp.uploads;
     return true;
 }
 
-// Sets the plan's tile order (hot slots, tile profile) for a launch of kernel `kern`; true when this
+// Sets the plan's tile order (slot list, tile profile) for a launch of kernel `kern`; true when this
 // launch is profiled (the caller copies the durations back after it).
 bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t st) {
     KParams& k = L.k;
     k.tiles_x = L.gx;
-    L.cold_rows = L.gy;
-    k.hot_rows = k.hot_n = 0;
+    k.hot = nullptr;
+    k.hot_n = 0;
     k.tile_cost = nullptr;
-    k.xterms = nullptr;
-    k.xcount = nullptr;
-    memset(k.hot_row_bits, 0, sizeof k.hot_row_bits);
     // (RRTE_DEBUG bit 5 runs one workgroup in image-order numbering: no tile order; bit 4's per-wave
-    // stamps work with it, a split tile's parts in their own slots)
-    if (!c->env_tile_order || c->env_wg256 || L.gy > 32u * kHotRowWords || L.gx > 0xfffu || (k.debug & 32u))
-        return false;
+    // stamps work with it)
+    if (!c->env_tile_order || c->env_wg256 || L.gx > 0xffffu || L.gy > 0xffffu || (k.debug & 32u)) return false;
     auto& tp = c->tprof;
     std::string key(reinterpret_cast<const char*>(&kern), sizeof kern);
     const uint32_t shape[] = {k.width, k.height, k.rows, k.row0, k.band_rows, k.nranks, k.rank, k.spp, k.max_depth,
                               (uint32_t)L.mode, (uint32_t)L.cull, (uint32_t)L.single};
     key.append(reinterpret_cast<const char*>(shape), sizeof shape);
     const uint32_t tiles = L.gx * L.gy;
-    const uint32_t parts = split_parts(c, L, k.light_part);
     if (tp.pending && hipEventQuery(tp.ev) == hipSuccess) {
         tp.pending = false;
         if (tp.pending_key == key) {
             // the order is composed on a worker thread from a copy of the durations: a whole frame's
-            // counting sort and slot list take ~0.5 ms of host time that a render call must not stall for
+            // counting sort takes ~0.5 ms of host time that a render call must not stall for
             std::vector<uint32_t> costs(tp.h_cost, tp.h_cost + tp.tiles);
-            const uint32_t n = tp.tiles, tx = tp.tiles_x;
-            const bool lpt = tp.lpt;
-            const double frac = c->split_frac;
-            tp.work = std::async(std::launch::async, [key, costs = std::move(costs), n, tx, lpt, parts, frac]() {
-                rrte_ctx::TileProfile w;
-                w.h_cost = const_cast<uint32_t*>(costs.data());
-                w.tiles = n;
-                w.tiles_x = tx;
-                w.lpt = lpt;
-                build_hot_list(w);
-                compose_slots(w, parts, tx, n, frac);
-                TilePlanResult r;
-                r.key = key;
-                r.top = std::move(w.top);
-                r.top_max = w.top_max;
-                r.slots = std::move(w.slots);
-                memcpy(r.row_bits, w.row_bits, sizeof r.row_bits);
-                r.has_split = w.has_split;
-                r.parts = parts;
-                w.h_cost = nullptr;
-                return r;
+            const uint32_t tx = tp.tiles_x;
+            tp.work = std::async(std::launch::async, [key, costs = std::move(costs), tx]() {
+                return TilePlanResult{key, lpt_slots(costs.data(), (uint32_t)costs.size(), tx)};
             });
             tp.working = true;
             tp.launches = 0;
@@ -1284,45 +1260,45 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     if (tp.working && tp.work.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
         TilePlanResult r = tp.work.get();
         tp.working = false;
-        if (r.key == key) {  // (a result for another shape is dropped)
+        if (r.key == key && r.slots.size() == tiles) {  // (a result for another shape is dropped)
             tp.key = key;
-            tp.top = std::move(r.top);
-            tp.top_max = r.top_max;
             tp.slots = std::move(r.slots);
-            memcpy(tp.row_bits, r.row_bits, sizeof tp.row_bits);
-            tp.has_split = r.has_split;
-            tp.slots_parts = r.parts;
             tp.fixed = false;
+            if (tp.cur >= 0 && retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
             tp.cur = -1;
         }
     }
     if (tp.key != key) {  // another shape: drop the list, profile as soon as the copy buffer is free
         tp.key = key;
-        tp.top.clear();
         tp.slots.clear();
-        tp.slots_parts = 0;
         tp.fixed = c->env_tile_order_fixed;
-        tp.lpt = c->env_tile_order_lpt;
+        if (tp.fixed) tp.slots = fixed_slots(tiles, L.gx);
+        if (tp.cur >= 0 && retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
+        tp.cur = -1;
         tp.launches = kTileReprofile;
     }
     if (tp.fixed) tp.launches = 0;  // RRTE_TILE_ORDER=2: the fixed list, never profiled
     // a moving camera moves the expensive tiles: re-profile after kTileReprofileMoving launches instead
     const uint64_t cam = fnv1a(&k.cam[0], offsetof(FrameCam, tile_cull));
     const bool moved = cam != tp.cam_sig;
-    const bool profile = !tp.pending && (tp.launches >= kTileReprofile || (moved && tp.launches >= kTileReprofileMoving));
+    const uint64_t every = c->env_test_recycle ? 1 : kTileReprofile, moving = c->env_test_recycle ? 1 : kTileReprofileMoving;
+    const bool profile = !tp.pending && (tp.launches >= every || (moved && tp.launches >= moving));
     ++tp.launches;
-    if ((!tp.top.empty() || tp.fixed) && (tp.slots_parts != parts || tp.slots.empty())) compose_slots(tp, parts, L.gx, tiles, c->split_frac);
-    if (!tp.slots.empty() && (tp.cur >= 0 || upload_hot_list(c, L.gy))) {
+    // RRTE_TEST_RECYCLE=1: a new list version every launch (the fixed list re-uploaded), so the
+    // version pool wraps within kVersions launches
+    if (c->env_test_recycle && tp.fixed && tp.cur >= 0) {
+        if (retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
+        tp.cur = -1;
+    }
+    if (!tp.slots.empty() && tp.slots.size() == tiles && (tp.cur >= 0 || upload_hot_list(c))) {
         k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
-        k.hot_rows = (k.hot_n + L.gx - 1) / L.gx;
-        memcpy(k.hot_row_bits, tp.row_bits, sizeof tp.row_bits);
-        L.cold_rows = tp.lpt ? 0u : L.gy;  // an LPT list covers every tile: no image-order rows
+        tp.ret[tp.cur].use(st);
     }
     if (!profile) return false;
     if (ensure(c, tp.d_cost, tp.cap_d, tiles) != RRTE_OK) return false;
     if (tp.cap_h < tiles) {
-        if (tp.h_cost) (void)hipHostFree(tp.h_cost);
+        if (tp.h_cost) (void)hipHostFree(tp.h_cost);  // (no copy into it is pending: !tp.pending)
         tp.h_cost = nullptr;
         tp.cap_h = 0;
         if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_cost), tiles * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
@@ -1330,9 +1306,8 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         tp.cap_h = tiles;
     }
     if (!tp.ev && hipEventCreateWithFlags(&tp.ev, hipEventDisableTiming) != hipSuccess) return false;
-    if (!reserve_hot_lists(c, std::max<size_t>(kHotListWords, (size_t)tiles + kMaxHotTiles))) return false;
-    if (hipMemsetAsync(tp.d_cost, 0, tiles * sizeof(uint32_t), st) != hipSuccess) return false;  // atomicMax per tile
-    k.tile_cost = tp.d_cost;
+    if (!reserve_hot_lists(c, tiles)) return false;
+    k.tile_cost = tp.d_cost;  // every tile of frame 0 stores its duration (no clearing needed)
     tp.cam_sig = cam;
     tp.pending_key = key;
     tp.tiles = tiles;
@@ -1340,59 +1315,9 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     return true;
 }
 
-// The exchange area of a launch with split tiles (KParams::xterms / xcount); nullptr-free on success.
-rrte_status plan_split_area(rrte_ctx* c, LaunchPlan& L, hipStream_t st, int& area) {
-    area = -1;
-    KParams& k = L.k;
-    if (!k.hot_n || !c->tprof.has_split) return RRTE_OK;
-    area = c->xnext;
-    c->xnext = (c->xnext + 1) % rrte_ctx::kXAreas;
-    auto& xa = c->xarea[area];
-    // split groups sit in the first kMaxHotTiles slots (compose_slots), whatever the list's length
-    const size_t groups = (size_t)std::min<uint32_t>(k.hot_n, kMaxHotTiles) * k.nframes;
-    const size_t terms = groups * k.num_lights * 3u * 64u;
-    if (xa.cap_terms < terms || xa.cap_count < groups) {
-        // every area of the ring at once, sized for the
-        // largest launch (kMaxHotTiles slots x kMaxLaunchFrames frames) of this light count: one device
-        // synchronisation at the first split launch, none later
-        HIPCHK(c, hipDeviceSynchronize());
-        const size_t gmax = (size_t)kMaxHotTiles * kMaxLaunchFrames, tmax = gmax * k.num_lights * 3u * 64u;
-        for (auto& a : c->xarea) {
-            if (a.terms) (void)hipFree(a.terms);
-            if (a.count) (void)hipFree(a.count);
-            a.terms = nullptr;
-            a.count = nullptr;
-            a.cap_terms = a.cap_count = 0;
-            HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&a.terms), tmax * sizeof(float)));
-            HIPCHK(c, hipMalloc(reinterpret_cast<void**>(&a.count), gmax * sizeof(uint32_t)));
-            HIPCHK(c, hipMemset(a.count, 0, gmax * sizeof(uint32_t)));
-            a.cap_terms = tmax;
-            a.cap_count = gmax;
-            a.used = false;
-        }
-    }
-    if (!xa.ev) HIPCHK(c, hipEventCreateWithFlags(&xa.ev, hipEventDisableTiming));
-    if (c->env_split_noevent) {  // RRTE_SPLIT_NOEVENT=1: timing only, the ring is reused untracked
-        k.xterms = xa.terms;
-        k.xcount = xa.count;
-        area = -1;
-        return RRTE_OK;
-    }
-    if (xa.used && hipEventQuery(xa.ev) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(st, xa.ev, 0));
-    k.xterms = xa.terms;
-    k.xcount = xa.count;
-    return RRTE_OK;
-}
-
-// Queues the profiled launch's copy-back on its stream (plan_tile_order returned true) and marks the
-// launch's split exchange area busy until the launch completes.
-rrte_status finish_tile_order(rrte_ctx* c, const LaunchPlan& L, bool profile, int area, hipStream_t st) {
+// Queues the profiled launch's copy-back on its stream (plan_tile_order returned true).
+rrte_status finish_tile_order(rrte_ctx* c, bool profile, hipStream_t st) {
     auto& tp = c->tprof;
-    (void)L;
-    if (area >= 0) {
-        HIPCHK(c, hipEventRecord(c->xarea[area].ev, st));
-        c->xarea[area].used = true;
-    }
     if (!profile) return RRTE_OK;
     HIPCHK(c, hipMemcpyAsync(tp.h_cost, tp.d_cost, (size_t)tp.tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipEventRecord(tp.ev, st));
@@ -1406,12 +1331,12 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     Cull cl{L.cull ? c->d_bounds : nullptr, L.num_prims};
     JitKernel* jk = jit_kernel_for(c, L.mode, L.cull, L.single);
     c->stats.jit_active = jk ? (jk->topology ? 2u : 1u) : 0u;
-    // 64-thread workgroups: (tile column, frame, hot rows + tile rows), KParams::hot
+    // 64-thread workgroups: (tile column, frame, tile row or slot row), KParams::hot
     const bool profile = plan_tile_order(c, L, jk ? (const void*)jk->fn : nullptr, st);
-    int area = -1;
-    if (rrte_status r = plan_split_area(c, L, st, area); r != RRTE_OK) return r;
     c->stats.hot_tiles = L.k.hot_n;
-    const dim3 grid(L.gx, L.k.nframes, L.k.hot_rows + L.cold_rows), block(kBlockThreads);
+    if (c->sb_cur >= 0) c->sb[c->sb_cur].ret.use(st);  // the launch reads the current scene version
+    c->launched.use(st);
+    const dim3 grid(L.gx, L.k.nframes, L.gy), block(kBlockThreads);
     if (jk) {
         unsigned long long* ctr = c->d_counters;
         MeshView mv = c->mesh_view;
@@ -1424,7 +1349,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         else
             HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, st, args, nullptr));
         hs.lap(8);
-        return finish_tile_order(c, L, profile, area, st);
+        return finish_tile_order(c, profile, st);
     }
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
                  c->mesh_view};
@@ -1436,7 +1361,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     else
         hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     HIPCHK(c, hipGetLastError());
-    return finish_tile_order(c, L, profile, area, st);
+    return finish_tile_order(c, profile, st);
 }
 
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
@@ -1561,12 +1486,9 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
-        c->env_tile_order_fixed = g[0] == '2';
-        c->env_tile_order_lpt = g[0] == '3';  // 0 image order, 1 hot list, 2 fixed list (tests), 3 LPT (default)
+        c->env_tile_order_fixed = g[0] == '2';  // 0 image order, 2 fixed permutation (tests), else measured (default)
     }
-    if (const char* g = getenv("RRTE_TILE_SPLIT")) c->env_tile_split = g[0] == '1';
-    if (const char* g = getenv("RRTE_SPLIT_FRAC"); g && *g) c->split_frac = strtod(g, nullptr);
-    if (const char* g = getenv("RRTE_SPLIT_NOEVENT")) c->env_split_noevent = g[0] == '1';
+    if (const char* g = getenv("RRTE_TEST_RECYCLE")) c->env_test_recycle = g[0] == '1';
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
@@ -1610,15 +1532,26 @@ void rrte_hip_destroy(rrte_ctx* c) {
     }
     (void)hipSetDevice(c->device);
     if (c->h_stall) __hip_atomic_store(c->h_stall, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // injected stall
-    (void)hipDeviceSynchronize();  // frames may still run on caller streams
+    // gathers first, bounded (a dead peer aborts the communicator instead of hanging here); then the
+    // frames that may still run on caller streams
+    if (c->comm && wait_bounded(c) != RRTE_OK) c->comm = nullptr;  // (comm_abort has aborted it)
+    (void)hipDeviceSynchronize();
     if (c->comm) ncclCommDestroy(c->comm);
     c->jit_pending.clear();  // joins background compiles
     for (auto& kv : c->jit_cache) jit_release(kv.second);
-    void* bufs[] = {c->d_prims,      c->d_mats,      c->d_lights,     c->d_nodes,     c->d_bounds,
-                    c->d_rgba,       c->d_f32,       c->d_counters,   c->d_gather,    c->d_full,
-                    c->d_mesh_nodes, c->d_mesh_tris, c->d_mesh_norms, c->d_mesh_perm};
+    for (auto& B : c->sb) {
+        void* sbufs[] = {B.d_prims, B.d_mats, B.d_lights, B.d_nodes, B.d_bounds, B.d_mesh_nodes, B.d_mesh_tris,
+                         B.d_mesh_norms, B.d_mesh_perm};
+        for (void* b : sbufs)
+            if (b) (void)hipFree(b);
+        destroy_events(B.ret);
+    }
+    void* bufs[] = {c->d_rgba, c->d_f32, c->d_counters, c->d_gather, c->d_full};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    for (void* b : c->graveyard)
+        if (b) (void)hipFree(b);
+    destroy_events(c->launched);
     for (uint32_t* b : c->d_slab)
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
@@ -1628,14 +1561,11 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->tprof.ev) (void)hipEventDestroy(c->tprof.ev);
     for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i) {
         if (c->tprof.d_list[i]) (void)hipFree(c->tprof.d_list[i]);
+        destroy_events(c->tprof.ret[i]);
     }
     if (c->tprof.h_list) (void)hipHostFree(c->tprof.h_list);
     if (c->tprof.upload_stream) (void)hipStreamDestroy(c->tprof.upload_stream);
-    for (auto& xa : c->xarea) {
-        if (xa.terms) (void)hipFree(xa.terms);
-        if (xa.count) (void)hipFree(xa.count);
-        if (xa.ev) (void)hipEventDestroy(xa.ev);
-    }
+    if (c->upload_stream) (void)hipStreamDestroy(c->upload_stream);
     for (hipEvent_t e : c->ev_poll)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1710,7 +1640,13 @@ rrte_status rrte_hip_synchronize(rrte_ctx* c) {
     rrte_status r = render_batch(c, false);
     if (r != RRTE_OK) return r;
     if ((r = wait_bounded(c)) != RRTE_OK) return r;
+    // every stream that launched a frame (bounded: a frame may sit behind a gather), then the device
+    if ((r = retire(c, c->launched)) != RRTE_OK || (r = wait_retired(c, c->launched)) != RRTE_OK) return r;
     HIPCHK(c, hipDeviceSynchronize());
+    // idle: buffers replaced while frames were in flight can go, and every retired version is free
+    for (void* b : c->graveyard)
+        if (b) (void)hipFree(b);
+    c->graveyard.clear();
     return finish_frame(c);
 }
 
@@ -1762,22 +1698,20 @@ rrte_status rrte_hip_sdf_guards(const rrte_sdf_node* in, uint32_t count, uint32_
     return RRTE_OK;
 }
 
-rrte_status rrte_hip_tile_order_plan(const uint32_t* costs, uint32_t tiles, uint32_t tiles_x, int lpt, uint32_t parts,
-                                     double split_frac, uint32_t* slots, uint32_t cap, uint32_t* n_slots) {
-    if (!costs || !slots || !n_slots || tiles == 0 || tiles_x == 0 || tiles_x > 0xfffu || parts < 1 || parts > 4)
+rrte_status rrte_hip_tile_order_plan(const uint32_t* costs, uint32_t tiles, uint32_t tiles_x, uint32_t* slots,
+                                     uint32_t cap, uint32_t* n_slots) {
+    if (!costs || !slots || !n_slots || tiles == 0 || tiles_x == 0 || tiles_x > 0xffffu || tiles / tiles_x > 0xffffu)
         return RRTE_INVALID_ARG;
-    rrte_ctx::TileProfile tp;
-    std::vector<uint32_t> h(costs, costs + tiles);
-    tp.h_cost = h.data();
-    tp.tiles = tiles;
-    tp.tiles_x = tiles_x;
-    tp.lpt = lpt != 0;
-    build_hot_list(tp);
-    compose_slots(tp, parts, tiles_x, tiles, split_frac);
-    tp.h_cost = nullptr;  // not owned
-    *n_slots = (uint32_t)tp.slots.size();
-    if (tp.slots.size() > cap) return RRTE_INVALID_ARG;
-    std::copy(tp.slots.begin(), tp.slots.end(), slots);
+    const std::vector<uint32_t> v = lpt_slots(costs, tiles, tiles_x);
+    *n_slots = (uint32_t)v.size();
+    if (v.size() > cap) return RRTE_INVALID_ARG;
+    std::copy(v.begin(), v.end(), slots);
+    return RRTE_OK;
+}
+
+rrte_status rrte_hip_jit_cache_key(const char* source, const char* headers_override, char* out, size_t out_len) {
+    if (!source || !out || out_len < 33) return RRTE_INVALID_ARG;
+    snprintf(out, out_len, "%s", jit_cache_name(source, headers_override).c_str());
     return RRTE_OK;
 }
 
@@ -1866,7 +1800,9 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
     rrte_status fr = c->comm ? flush_batch(c) : RRTE_OK;
     c->batch.n = c->batch.nsrc = c->batch.rendered = 0;
     if (fr == RRTE_OK && c->comm) fr = wait_bounded(c);
-    HIPCHK(c, hipDeviceSynchronize());
+    if (fr == RRTE_OK) {  // the frames on caller streams too (bounded)
+        if ((fr = retire(c, c->launched)) == RRTE_OK) fr = wait_retired(c, c->launched);
+    }
     if (c->comm) ncclCommDestroy(c->comm);
     c->comm = nullptr;
     c->last_gather_stream = nullptr;
@@ -1877,7 +1813,23 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
     if (fr != RRTE_OK) return fr;
     ncclUniqueId id;
     memcpy(&id, id_bytes, sizeof id);
-    NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    // Non-blocking initialisation, polled under the same timeout as every gather wait: a peer that
+    // never joins surfaces as RRTE_RCCL_ERROR instead of a hang in ncclCommInitRank.  (Every later call
+    // on the communicator may then return ncclInProgress: nccl_settle.)
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const ncclResult_t ir = ncclCommInitRankConfig(&c->comm, nranks, id, rank, &cfg);
+    if (ir != ncclSuccess && ir != ncclInProgress) {
+        if (c->comm) (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+        return fail(c, RRTE_RCCL_ERROR, "ncclCommInitRankConfig failed: %s", ncclGetErrorString(ir));
+    }
+    if (rrte_status r = nccl_settle(c, ir, "ncclCommInitRankConfig"); r != RRTE_OK) {
+        if (c->comm) (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+        c->comm_failed = false;  // (no communicator: a later comm_init starts clean)
+        return r;
+    }
     c->nranks = nranks;
     c->rank = rank;
     if (nranks == 1 && c->emu_nranks > 1) {
@@ -1998,6 +1950,26 @@ static rrte_status before_collective(rrte_ctx* c, hipStream_t st) {
     return RRTE_OK;
 }
 
+// A call on the non-blocking communicator returned `r`: ncclInProgress means RCCL is still setting the
+// operation up (connections, the communicator itself), and the next call may only follow once the
+// communicator's state has left ncclInProgress -- polled under comm_timeout_ms.
+static rrte_status nccl_settle(rrte_ctx* c, ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return RRTE_OK;
+    if (r != ncclInProgress) return fail(c, RRTE_RCCL_ERROR, "%s failed: %s", what, ncclGetErrorString(r));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        ncclResult_t st = ncclInProgress;
+        if (ncclCommGetAsyncError(c->comm, &st) != ncclSuccess)
+            return fail(c, RRTE_RCCL_ERROR, "%s: ncclCommGetAsyncError failed", what);
+        if (st == ncclSuccess) return RRTE_OK;
+        if (st != ncclInProgress) return fail(c, RRTE_RCCL_ERROR, "%s failed: %s", what, ncclGetErrorString(st));
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->comm_timeout_ms))
+            return fail(c, RRTE_RCCL_ERROR, "%s did not complete within %u ms (a peer never joined?)", what,
+                        c->comm_timeout_ms);
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
 // A gather failed or did not finish in time: release any injected stall, give the queued work a short
 // bounded chance to drain (so nothing of this communicator is still running when it is torn down),
 // abort the communicator and fail every later gather call until rrte_hip_comm_init.
@@ -2023,27 +1995,19 @@ static rrte_status comm_abort(rrte_ctx* c, const char* why) {
     return fail(c, RRTE_RCCL_ERROR, "%s; communicator aborted (call rrte_hip_comm_init again)", why);
 }
 
-// Bounded wait for the context's own streams and its last gather: polls the events (and, while a
-// communicator exists, ncclCommGetAsyncError) instead of blocking, so a gather that never completes
-// -- a dead or stalled peer -- surfaces as RRTE_RCCL_ERROR after comm_timeout_ms instead of a hang.
-static rrte_status wait_bounded(rrte_ctx* c) {
-    constexpr int kPoll = 3 + rrte_ctx::kBatchSlabs;
-    static_assert(sizeof(c->ev_poll) / sizeof(c->ev_poll[0]) == kPoll, "poll events");
-    hipStream_t ss[kPoll] = {c->stream, c->comm_stream, c->last_gather_stream};
-    for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i) ss[3 + i] = c->render_stream[i];
-    int n = 0;
-    for (int i = 0; i < kPoll; ++i) {
-        if (!ss[i]) continue;
-        if (!c->ev_poll[n]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_poll[n], hipEventDisableTiming));
-        HIPCHK(c, hipEventRecord(c->ev_poll[n], ss[i]));
-        ++n;
-    }
-    const bool watch = c->comm != nullptr;
+// Bounded wait for events: polls them (and, while a communicator exists, ncclCommGetAsyncError)
+// instead of blocking, so work that sits behind a gather that never completes -- a dead or stalled
+// peer -- surfaces as RRTE_RCCL_ERROR after comm_timeout_ms (the communicator aborted) instead of a
+// hang.  Without a communicator no gather can stall a frame (an aborted one's kernels are being torn
+// down), but the wait stays bounded all the same: RRTE_HIP_ERROR after kNoCommWaitMs.
+constexpr uint32_t kNoCommWaitMs = 60000;
+static rrte_status poll_events(rrte_ctx* c, const hipEvent_t* ev, size_t n) {
     const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t limit_ms = c->comm ? c->comm_timeout_ms : std::max(c->comm_timeout_ms, kNoCommWaitMs);
     for (uint32_t spin = 0;; ++spin) {
         bool busy = false;
-        for (int i = 0; i < n; ++i) {
-            const hipError_t e = hipEventQuery(c->ev_poll[i]);
+        for (size_t i = 0; i < n; ++i) {
+            const hipError_t e = hipEventQuery(ev[i]);
             if (e == hipErrorNotReady) {
                 busy = true;
                 break;
@@ -2051,21 +2015,40 @@ static rrte_status wait_bounded(rrte_ctx* c) {
             HIPCHK(c, e);
         }
         if (!busy) return RRTE_OK;
-        if (watch) {
+        const bool late = std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(limit_ms);
+        if (c->comm) {
             ncclResult_t ae = ncclSuccess;
             if (ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
                 char why[256];
                 snprintf(why, sizeof why, "RCCL asynchronous error: %s", ncclGetErrorString(ae));
                 return comm_abort(c, why);
             }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->comm_timeout_ms)) {
+            if (late) {
                 char why[256];
                 snprintf(why, sizeof why, "gather did not complete within %u ms (stalled or dead peer?)", c->comm_timeout_ms);
                 return comm_abort(c, why);
             }
+        } else if (late) {
+            return fail(c, RRTE_HIP_ERROR, "device work did not complete within %u ms", limit_ms);
         }
         if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
+}
+
+// Bounded wait for the context's own streams and its last gather (poll_events).
+static rrte_status wait_bounded(rrte_ctx* c) {
+    constexpr int kPoll = 3 + rrte_ctx::kBatchSlabs;
+    static_assert(sizeof(c->ev_poll) / sizeof(c->ev_poll[0]) == kPoll, "poll events");
+    hipStream_t ss[kPoll] = {c->stream, c->comm_stream, c->last_gather_stream};
+    for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i) ss[3 + i] = c->render_stream[i];
+    size_t n = 0;
+    for (int i = 0; i < kPoll; ++i) {
+        if (!ss[i]) continue;
+        if (!c->ev_poll[n]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_poll[n], hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->ev_poll[n], ss[i]));
+        ++n;
+    }
+    return poll_events(c, c->ev_poll, n);
 }
 
 // Close the open batch (collective: every rank holds the same open batch -- same frames in the same
@@ -2159,7 +2142,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             int lo = 0, hi = 0;
             HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
             HIPCHK(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, c->env_comm_priority ? hi : lo));
-            for (int i = 0; i < rrte_ctx::kBatchSlabs; ++i) {
+            for (int i = 0; i < c->batch_slabs; ++i) {  // (only the slots of the ring in use)
                 HIPCHK(c, hipStreamCreateWithFlags(&c->render_stream[i], hipStreamNonBlocking));
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_batch[i], hipEventDisableTiming));
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_render[i], hipEventDisableTiming));
@@ -2187,9 +2170,10 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             // every rank holds a receive slab too (the root's is the only one written)
             const size_t send = (size_t)b.cap * slice, recv = send * (size_t)c->nranks;
             if (c->cap_bsend[k] < send || c->cap_brecv[k] < recv) {
-                // every slab of the ring at once (one device sync at the first batch, none in steady state)
-                HIPCHK(c, hipDeviceSynchronize());  // no render or gather may still use a slab being resized
-                for (int q = 0; q < rrte_ctx::kBatchSlabs; ++q) {
+                // every slab of the ring in use at once (at the first batch: none is allocated inside a
+                // later timed batch); a smaller slab an in-flight gather may still use goes to the
+                // graveyard (freed when the context is next idle), so nothing waits for the device here
+                for (int q = 0; q < c->batch_slabs; ++q) {
                     if ((r = ensure(c, c->d_bsend[q], c->cap_bsend[q], send)) != RRTE_OK) return r;
                     if ((r = ensure(c, c->d_brecv[q], c->cap_brecv[q], recv)) != RRTE_OK) return r;
                 }
@@ -2214,9 +2198,8 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         const int slot = (int)(c->gather_frames % rrte_ctx::kSlabs);
         const size_t slab_words = slice * (size_t)c->nranks / 4u;
         if (c->cap_slab[slot] < slab_words) {
-            // (re)size the whole ring at once: one device synchronisation (no slab may be freed under an
-            // in-flight gather) instead of one per slot spread over the first kSlabs frames
-            HIPCHK(c, hipDeviceSynchronize());
+            // (re)size the whole ring at once; smaller slabs in-flight gathers may still use go to the
+            // graveyard (freed when the context is next idle): no device synchronisation
             for (int i = 0; i < rrte_ctx::kSlabs; ++i)
                 if ((r = ensure(c, c->d_slab[i], c->cap_slab[i], slab_words)) != RRTE_OK) return r;
         }
@@ -2236,11 +2219,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         if ((r = before_collective(c, st)) != RRTE_OK) return comm_abort(c, ("gather setup failed: " + c->err).c_str());
         {
             const ncclResult_t nr = ncclGather(mine, slab, slice, ncclUint8, root, c->comm, st);
-            if (nr != ncclSuccess) {
-                char why[256];
-                snprintf(why, sizeof why, "ncclGather failed: %s", ncclGetErrorString(nr));
-                return comm_abort(c, why);
-            }
+            if (nr != ncclSuccess && nccl_settle(c, nr, "ncclGather") != RRTE_OK) return comm_abort(c, c->err.c_str());
         }
         hs.lap(5);
         if (c->rank == root) {

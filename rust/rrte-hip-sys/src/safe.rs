@@ -1,0 +1,172 @@
+//! Safe wrapper over the C ABI (the only `unsafe` code of the integration): an owned context, an
+//! owned lowered scene, owned frames.  rrte-renderer-hip (which keeps the workspace's
+//! `unsafe_code = "forbid"`) builds on this module only.
+//!
+//! Conventions of include/rrte_hip.h: the caller owns every buffer, the context owns device memory
+//! and streams, no panic or exception crosses the ABI, one context per thread (not internally
+//! synchronised: `&mut self` here), multi-GPU is internal to the context.
+use crate::*;
+use std::ffi::CStr;
+use std::fmt;
+
+/// A failed call: the status and the library's message (rrte_hip_last_error).
+#[derive(Debug, Clone, PartialEq, Eq)]
+pub struct Error {
+    pub status: rrte_status,
+    pub message: String,
+}
+
+impl fmt::Display for Error {
+    fn fmt(&self, f: &mut fmt::Formatter<'_>) -> fmt::Result {
+        let name = match self.status {
+            RRTE_INVALID_ARG => "INVALID_ARG",
+            RRTE_HIP_ERROR => "HIP_ERROR",
+            RRTE_RCCL_ERROR => "RCCL_ERROR",
+            RRTE_UNSUPPORTED_PRIM => "UNSUPPORTED_PRIM",
+            RRTE_NO_DEVICE => "NO_DEVICE",
+            _ => "UNKNOWN",
+        };
+        write!(f, "rrte_hip {name}: {}", self.message)
+    }
+}
+
+impl std::error::Error for Error {}
+
+/// A lowered scene: the arrays an `rrte_scene_ir` points into, owned by Rust.
+#[derive(Clone, Default)]
+pub struct SceneIr {
+    pub prims: Vec<rrte_prim>,
+    pub materials: Vec<rrte_material>,
+    pub lights: Vec<rrte_light>,
+    pub sdf_nodes: Vec<rrte_sdf_node>,
+    pub camera: rrte_camera,
+    pub mesh_vertices: Vec<rrte_mesh_vertex>,
+    pub mesh_indices: Vec<u32>,
+    /// Caller-maintained dirty stamp of the mesh arrays (0: compared byte for byte), the analogue of
+    /// Scene::is_dirty (crates/rrte-scene/src/lib.rs:310-312).
+    pub mesh_version: u64,
+}
+
+impl SceneIr {
+    /// The C view of the arrays; valid while `self` is neither moved nor modified.
+    fn raw(&self) -> rrte_scene_ir {
+        rrte_scene_ir {
+            prims: self.prims.as_ptr(),
+            num_prims: self.prims.len() as u32,
+            materials: self.materials.as_ptr(),
+            num_materials: self.materials.len() as u32,
+            lights: self.lights.as_ptr(),
+            num_lights: self.lights.len() as u32,
+            sdf_nodes: self.sdf_nodes.as_ptr(),
+            num_sdf_nodes: self.sdf_nodes.len() as u32,
+            camera: self.camera,
+            mesh_vertices: self.mesh_vertices.as_ptr(),
+            num_mesh_vertices: self.mesh_vertices.len() as u32,
+            mesh_indices: self.mesh_indices.as_ptr(),
+            num_mesh_indices: self.mesh_indices.len() as u32,
+            mesh_version: self.mesh_version,
+        }
+    }
+}
+
+/// One rrte_hip context on one HIP device.
+pub struct Context {
+    ctx: *mut rrte_ctx,
+}
+
+// A context may move between threads (it is used by one thread at a time: `&mut self`).
+unsafe impl Send for Context {}
+
+impl Context {
+    /// rrte_hip_create: a context on HIP device `device` (RRTE_NO_DEVICE without one).
+    pub fn new(device: i32) -> Result<Self, Error> {
+        let mut ctx: *mut rrte_ctx = std::ptr::null_mut();
+        let st = unsafe { rrte_hip_create(device, &mut ctx) };
+        if st != RRTE_OK || ctx.is_null() {
+            return Err(Error { status: st, message: "rrte_hip_create failed (no HIP device?)".into() });
+        }
+        if unsafe { rrte_hip_abi_version() } != RRTE_ABI_VERSION {
+            unsafe { rrte_hip_destroy(ctx) };
+            return Err(Error { status: RRTE_INVALID_ARG, message: "librrte_hip ABI version mismatch".into() });
+        }
+        Ok(Self { ctx })
+    }
+
+    fn check(&self, st: rrte_status) -> Result<(), Error> {
+        if st == RRTE_OK {
+            return Ok(());
+        }
+        let message = unsafe { CStr::from_ptr(rrte_hip_last_error(self.ctx)) }.to_string_lossy().into_owned();
+        Err(Error { status: st, message })
+    }
+
+    /// Raytracer::render on the GPU: a new W*H*4 RGBA8 buffer, row 0 = top (raytracer.rs:54-89).
+    pub fn render(&mut self, scene: &SceneIr, params: &rrte_render_params) -> Result<Vec<u8>, Error> {
+        let mut out = vec![0u8; params.width as usize * params.height as usize * 4];
+        self.render_into(scene, params, &mut out)?;
+        Ok(out)
+    }
+
+    /// The same into a caller buffer of at least W*H*4 bytes (Engine::frame_buffer, reused per frame).
+    pub fn render_into(&mut self, scene: &SceneIr, params: &rrte_render_params, out: &mut [u8]) -> Result<(), Error> {
+        let need = params.width as usize * params.height as usize * 4;
+        if out.len() < need {
+            return Err(Error { status: RRTE_INVALID_ARG, message: format!("output buffer {} < {need} bytes", out.len()) });
+        }
+        let ir = scene.raw();
+        let st = unsafe { rrte_hip_render(self.ctx, &ir, params, out.as_mut_ptr()) };
+        self.check(st)
+    }
+
+    /// Statistics of the last frame (rays cast, kernel time, gather time, upload time).
+    pub fn stats(&self) -> Result<rrte_stats, Error> {
+        let mut s = rrte_stats::default();
+        self.check(unsafe { rrte_hip_stats(self.ctx, &mut s) })?;
+        Ok(s)
+    }
+
+    /// Scene-specialised kernels: RRTE_JIT_OFF / RRTE_JIT_ON / RRTE_JIT_AUTO (default).
+    pub fn set_jit(&mut self, mode: c_int) -> Result<(), Error> {
+        self.check(unsafe { rrte_hip_set_jit(self.ctx, mode) })
+    }
+
+    /// Multi-GPU: the 128-byte unique id rank 0 creates and broadcasts out of band.
+    pub fn comm_unique_id() -> Result<[u8; RRTE_UNIQUE_ID_BYTES], Error> {
+        let mut id = [0u8; RRTE_UNIQUE_ID_BYTES];
+        let st = unsafe { rrte_hip_comm_unique_id(id.as_mut_ptr()) };
+        if st != RRTE_OK {
+            return Err(Error { status: st, message: "rrte_hip_comm_unique_id failed".into() });
+        }
+        Ok(id)
+    }
+
+    /// Joins the RCCL communicator (one process per GPU, every rank calls it).
+    pub fn comm_init(&mut self, nranks: i32, rank: i32, id: &[u8; RRTE_UNIQUE_ID_BYTES]) -> Result<(), Error> {
+        self.check(unsafe { rrte_hip_comm_init(self.ctx, nranks, rank, id.as_ptr()) })
+    }
+
+    /// Bounded waits: a gather that does not complete within `ms` aborts the communicator.
+    pub fn set_comm_timeout(&mut self, ms: u32) -> Result<(), Error> {
+        self.check(unsafe { rrte_hip_set_comm_timeout(self.ctx, ms) })
+    }
+
+    /// One frame over every rank: this rank's row bands, gathered to `root`, which gets the frame.
+    pub fn render_gather(&mut self, scene: &SceneIr, params: &rrte_render_params, root: i32, is_root: bool)
+                         -> Result<Option<Vec<u8>>, Error> {
+        let ir = scene.raw();
+        if is_root {
+            let mut out = vec![0u8; params.width as usize * params.height as usize * 4];
+            self.check(unsafe { rrte_hip_render_gather(self.ctx, &ir, params, root, out.as_mut_ptr()) })?;
+            Ok(Some(out))
+        } else {
+            self.check(unsafe { rrte_hip_render_gather(self.ctx, &ir, params, root, std::ptr::null_mut()) })?;
+            Ok(None)
+        }
+    }
+}
+
+impl Drop for Context {
+    fn drop(&mut self) {
+        unsafe { rrte_hip_destroy(self.ctx) };
+    }
+}

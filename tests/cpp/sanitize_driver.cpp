@@ -72,21 +72,22 @@ int main() {
     CHECK(rrte_hip_band_rows_for_rank(1080, 16, 8, 3) == 136u, "band rows (8 full bands + the 8-row last)");
     CHECK(rrte_hip_band_rows_for_rank(1080, 16, 8, 7) == 128u, "band rows last rank");
     {
-        // tile-order planning (the host code a context runs after a profile): hot list and LPT, with
-        // and without split tiles, on a 240 x 135 frame with a silhouette-like tail
+        // tile-order planning (the host code a context runs after a profile): every tile, slowest
+        // first, on a 240 x 135 frame with a silhouette-like tail; the JIT cache key with and without
+        // a header override
         const uint32_t tx = 240, n = 240 * 135;
-        std::vector<uint32_t> costs(n), slots(n + 2048);
+        std::vector<uint32_t> costs(n), slots(n + 16);
         for (uint32_t i = 0; i < n; ++i) costs[i] = 200u + (i * 2654435761u >> 20) % 3000u + (i % 97 == 0 ? 9000u : 0u);
-        for (int lpt = 0; lpt < 2; ++lpt)
-            for (uint32_t parts : {1u, 3u}) {
-                uint32_t got = 0;
-                CHECK(rrte_hip_tile_order_plan(costs.data(), n, tx, lpt, parts, 0.7, slots.data(), (uint32_t)slots.size(),
-                                               &got) == RRTE_OK, "tile order plan");
-                CHECK(lpt ? got >= n : (got > 0 && got <= 1024u), "tile order slot count %u", got);
-            }
         uint32_t got = 0;
-        CHECK(rrte_hip_tile_order_plan(costs.data(), n, tx, 1, 1, 0.7, slots.data(), 16, &got) == RRTE_INVALID_ARG,
+        CHECK(rrte_hip_tile_order_plan(costs.data(), n, tx, slots.data(), (uint32_t)slots.size(), &got) == RRTE_OK,
+              "tile order plan");
+        CHECK(got == n, "tile order slot count %u", got);
+        CHECK(rrte_hip_tile_order_plan(costs.data(), n, tx, slots.data(), 16, &got) == RRTE_INVALID_ARG,
               "tile order plan into a small buffer");
+        char k1[40], k2[40];
+        CHECK(rrte_hip_jit_cache_key("src", nullptr, k1, sizeof k1) == RRTE_OK &&
+                  rrte_hip_jit_cache_key("src", "hdr", k2, sizeof k2) == RRTE_OK && strcmp(k1, k2) != 0,
+              "jit cache key");
     }
     try {
         twist(Vec3(1.0f, 1.0f, 0.0f), 1.0f);

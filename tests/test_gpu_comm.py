@@ -145,3 +145,64 @@ def test_stalled_gather_surfaces_as_error(batch, monkeypatch):
     for i in range(2 * batch, 3 * batch):
         assert np.array_equal(outs[i].cpu().numpy().view(np.uint8), want[i]), f"frame {i}"
     ctx.close()
+
+
+def _animated_frames(n):
+    """Frames whose SCENE changes every frame (a light dimmed step by step): every frame call uploads
+    a new scene version."""
+    from rrte_amd.math import f32
+    out = []
+    for i in range(n):
+        objs, lights, cam, cfg = scenes.sdf_showcase(W, H)
+        lights[0].intensity = f32(25.0 - 0.5 * i)
+        out.append((LoweredScene(objs, lights, cam), cfg.lower()))
+    return out
+
+
+@pytest.mark.parametrize("what", ["tile_list_recycle", "scene_change"])
+def test_stall_during_recycle_or_scene_change_is_bounded(what, monkeypatch):
+    """while the 2nd collective is stalled, frames keep arriving that (a) recycle the
+    tile-list version pool every launch (RRTE_TEST_RECYCLE=1 with the fixed list) or (b) change the
+    scene every frame, so the scene-version ring wraps onto versions read by renders queued behind the
+    stalled gather.  Nothing may wait on the device unboundedly: (a) never waits at all (a version is
+    reused only once its readers completed; otherwise the launch keeps its list), (b) waits for the
+    version with the comm timeout.  The error surfaces as RRTE_RCCL_ERROR within the timeout, and
+    after rrte_hip_comm_init frames are exact again."""
+    import torch
+    monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    monkeypatch.setenv("RRTE_FAULT_STALL_GATHER", "2")
+    if what == "tile_list_recycle":
+        monkeypatch.setenv("RRTE_TILE_ORDER", "2")
+        monkeypatch.setenv("RRTE_TEST_RECYCLE", "1")
+        frames = _frames(30)
+    else:
+        frames = _animated_frames(30)
+    want = _want(frames[-3:])
+    ctx = Context(0, jit=abi.JIT_ON)
+    _comm(ctx)
+    ctx.check(ctx.lib.rrte_hip_set_comm_timeout(ctx.h, 300))
+    ctx.check(ctx.lib.rrte_hip_set_gather_batch(ctx.h, 3))
+    stream = torch.cuda.Stream()
+    outs = [torch.full((W * H,), -1, dtype=torch.int32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rc = abi.RRTE_OK
+    for (sc, prm), o in zip(frames[:27], outs):  # 9 batches: the 2nd one's gather stalls
+        rc = _gather(ctx, sc, prm, o, stream)
+        if rc != abi.RRTE_OK:
+            break
+    if rc == abi.RRTE_OK:
+        rc = ctx.lib.rrte_hip_synchronize(ctx.h)
+    dt = time.perf_counter() - t0
+    msg = ctx.lib.rrte_hip_last_error(ctx.h)
+    assert rc == abi.RRTE_RCCL_ERROR, (rc, msg)
+    assert b"did not complete within 300 ms" in msg and b"aborted" in msg, msg
+    assert dt < 4.0, dt  # the timeout, not the injected stall's own 5 s deadline
+    _comm(ctx)  # recovery (the injected fault is one-shot)
+    for (sc, prm), o in zip(frames[27:], outs[27:]):
+        ctx.check(_gather(ctx, sc, prm, o, stream))
+    ctx.check(ctx.lib.rrte_hip_flush(ctx.h))
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    for j, i in enumerate(range(27, 30)):
+        assert np.array_equal(outs[i].cpu().numpy().view(np.uint8), want[j]), f"frame {i}"
+    ctx.close()

@@ -1,19 +1,18 @@
-"""Hot-first tile order and split hot tiles (KParams::hot, rrte_hip.hip plan_tile_order): a launch
-may dispatch a list of tiles first and skip them in image order, and a hot tile may be rendered as
-one workgroup per shadow-casting light, the last of which sums the lights' terms in light order.
-Pixels are independent (raytracer.rs:57-60) and adding a light that contributes nothing as +0 is
-exact, so every order and split must give the same bytes, linear floats and shadow-ray counts as
-image order.  RRTE_TILE_ORDER=2 forces a fixed list of tiles spread over the frame (first and last
-tile included, every other one split when RRTE_TILE_SPLIT=1 and splitting applies) on every launch,
-so these tests run the hot slots, split parts, the partial hot row and the image-order skip on every
-kernel kind, mode and launch shape; RRTE_TILE_ORDER=0 is image order.  The default measures the tiles
-on a profiled launch and, once the durations arrive, dispatches every tile slowest first
-(RRTE_TILE_ORDER=3; =1 only the 1024 slowest first; no splits by default: measured slower)."""
+"""Measured-cost tile order (KParams::hot, rrte_hip.hip plan_tile_order): a launch may dispatch its
+tiles in any order -- the default measures every tile on a profiled launch and, once the durations
+arrive, dispatches every tile slowest first.  Pixels are independent (raytracer.rs:57-60), so every
+order must give the same bytes, linear floats and shadow-ray counts as image order.
+RRTE_TILE_ORDER=2 forces a fixed scrambled permutation of the tiles on every launch (no profile), so
+these tests run the list path on every kernel kind, mode and launch shape; RRTE_TILE_ORDER=0 is image
+order.  The timed configuration itself -- the default policy with 4 frames in flight at 1080p and 4K,
+after the measured list has landed -- is checked against the ORACLE."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
 
+import oracle
 from rrte_amd import LoweredScene, abi, scenes
 from rrte_amd.math import vec3
 from rrte_amd.renderer import Context
@@ -24,11 +23,14 @@ pytestmark = pytest.mark.gpu
 
 
 def _ctx(monkeypatch, order, jit, **env):
-    monkeypatch.setenv("RRTE_TILE_ORDER", order)
+    if order is None:
+        monkeypatch.delenv("RRTE_TILE_ORDER", raising=False)
+    else:
+        monkeypatch.setenv("RRTE_TILE_ORDER", order)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     ctx = Context(0, jit=jit)
-    monkeypatch.delenv("RRTE_TILE_ORDER")
+    monkeypatch.delenv("RRTE_TILE_ORDER", raising=False)
     for k in env:
         monkeypatch.delenv(k)
     return ctx
@@ -52,20 +54,9 @@ def _render(ctx, sc, prm, rows=None):
     return (rgba.cpu().numpy().view(np.uint8), f32.cpu().numpy().view(np.uint32), s1.shadow_rays, s1.hot_tiles)
 
 
-MAX_SLOTS = 1024  # device_scene.hpp kMaxHotTiles
-
-
-def _fixed_slots(tiles, parts):
-    """Slots of RRTE_TILE_ORDER=2's list (rrte_hip.hip compose_slots): m tiles, every other one split."""
-    m = min(tiles, MAX_SLOTS)
-    while m > 1 and (m + 1) // 2 * parts + m // 2 > MAX_SLOTS:
-        m -= 1
-    return (m + 1) // 2 * parts + m // 2
-
-
 SCENES = dict(scenes.SCENES, **{"all-lights": se.all_lights_scene, "mixed": se.mixed_scene})
-# (scene, W, H, mode, spp): 3 lights (3 parts), 5 point lights (4 parts, round robin), point +
-# directional + spot + ambient (3 parts, ambient in part 0), odd sizes, REFCOMPAT (never split)
+# (scene, W, H, mode, spp): odd sizes (a partial last slot row), every light kind, REFCOMPAT with
+# samples and bounces, the deformer and mesh kernels
 CASES = [("sdf-showcase", 320, 200, "lambert_shadow", 1), ("sdf-showcase", 162, 90, "lambert_shadow", 1),
          ("advanced-demo", 200, 120, "lambert_shadow", 1), ("all-lights", 120, 72, "lambert_shadow", 1),
          ("mixed", 96, 64, "lambert_shadow", 1), ("sdf-showcase", 96, 64, "refcompat", 3),
@@ -74,7 +65,7 @@ CASES = [("sdf-showcase", 320, 200, "lambert_shadow", 1), ("sdf-showcase", 162, 
 
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
 @pytest.mark.parametrize("name,w,h,mode,spp", CASES)
-def test_fixed_hot_list_is_exact(name, w, h, mode, spp, jit, monkeypatch):
+def test_fixed_tile_list_is_exact(name, w, h, mode, spp, jit, monkeypatch):
     objs, lights, cam, cfg = SCENES[name](w, h, mode=mode)
     if spp > 1:
         cfg.samples_per_pixel, cfg.max_depth, cfg.jitter = spp, 5, "random"
@@ -83,23 +74,20 @@ def test_fixed_hot_list_is_exact(name, w, h, mode, spp, jit, monkeypatch):
     a = _render(ref, sc, prm)
     assert a[3] == 0
     tiles = ((w + 7) // 8) * ((h + 7) // 8)
-    casters = sum(1 for lt in sc.lights[:sc.ir.num_lights] if lt.kind != abi.LIGHT_AMBIENT)
-    for split in ("0", "1"):
-        hot = _ctx(monkeypatch, "2", jit, RRTE_TILE_SPLIT=split)
-        b = _render(hot, sc, prm)
-        parts = min(casters, 4) if split == "1" and mode == "lambert_shadow" and spp == 1 else 1
-        assert b[3] == _fixed_slots(tiles, parts if parts > 1 else 1)
-        assert np.array_equal(a[0], b[0]), (split, (a[0] != b[0]).sum())
-        assert np.array_equal(a[1], b[1]), split
-        assert a[2] == b[2], split
-        hot.close()
+    hot = _ctx(monkeypatch, "2", jit)
+    b = _render(hot, sc, prm)
+    assert b[3] == tiles
+    assert np.array_equal(a[0], b[0]), (a[0] != b[0]).sum()
+    assert np.array_equal(a[1], b[1])
+    assert a[2] == b[2]
+    hot.close()
     ref.close()
 
 
 @pytest.mark.parametrize("nranks,rank", [(3, 1), (8, 0), (8, 7)])
-def test_fixed_hot_list_on_band_mapped_ranks(nranks, rank, monkeypatch):
-    """One rank's packed interleaved bands (RRTE_EMULATE_RANK): hot tiles address the rank's local
-    tile rows, the camera-tile mask maps them to image rows."""
+def test_fixed_tile_list_on_band_mapped_ranks(nranks, rank, monkeypatch):
+    """One rank's packed interleaved bands (RRTE_EMULATE_RANK): slots address the rank's local tile
+    rows, the camera-tile mask maps them to image rows."""
     w, h, band = 256, 200, 16
     objs, lights, cam, cfg = scenes.sdf_showcase(w, h)
     cfg.band_rows = band
@@ -109,27 +97,13 @@ def test_fixed_hot_list_on_band_mapped_ranks(nranks, rank, monkeypatch):
     ref = _ctx(monkeypatch, "0", abi.JIT_ON, **env)
     hot = _ctx(monkeypatch, "2", abi.JIT_ON, **env)
     a, b = _render(ref, sc, prm, rows), _render(hot, sc, prm, rows)
-    assert b[3] > 0
+    assert b[3] == 32 * ((rows + 7) // 8)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
     ref.close()
     hot.close()
 
 
-def test_fixed_hot_list_at_4k(monkeypatch):
-    """BASELINE configs[3]'s size: 480 x 270 tiles (270 tile rows: the row bitmap's upper words) and
-    16x16 camera-culling blocks."""
-    objs, lights, cam, cfg = scenes.sdf_showcase(3840, 2160)
-    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
-    ref = _ctx(monkeypatch, "0", abi.JIT_ON)
-    hot = _ctx(monkeypatch, "2", abi.JIT_ON, RRTE_TILE_SPLIT="1")
-    a, b = _render(ref, sc, prm), _render(hot, sc, prm)
-    assert b[3] == _fixed_slots(480 * 270, 3)  # 3 lights: 256 split tiles of 3 parts + 256 whole ones
-    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
-    ref.close()
-    hot.close()
-
-
-def test_measured_hot_list(monkeypatch):
+def test_measured_order(monkeypatch):
     """The default policy: the first launch of a shape is profiled, the durations come back
     asynchronously and a later launch dispatches every tile in measured-cost order; every frame on
     the way is identical to image order."""
@@ -138,20 +112,19 @@ def test_measured_hot_list(monkeypatch):
     ref = _ctx(monkeypatch, "0", abi.JIT_ON)
     want = _render(ref, sc, prm)
     ref.close()
-    monkeypatch.delenv("RRTE_TILE_ORDER", raising=False)
-    ctx = Context(0, jit=abi.JIT_ON)
+    ctx = _ctx(monkeypatch, None, abi.JIT_ON)
     seen = 0
     for _ in range(6):
         got = _render(ctx, sc, prm)
         assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[2]
         seen = max(seen, got[3])
-    assert seen == 80 * 45  # the default whole-frame order: one slot per tile
+    assert seen == 80 * 45  # one slot per tile
     ctx.close()
 
 
-def test_fixed_hot_list_in_batched_gathers(monkeypatch):
-    """Multi-frame launches of the batched gather path (blockIdx.y = frame): every frame's hot tiles
-    first, 8 frames per launch, a partial last batch."""
+def test_fixed_tile_list_in_batched_gathers(monkeypatch):
+    """Multi-frame launches of the batched gather path (blockIdx.y = frame): every frame's slots, 8
+    frames per launch, a partial last batch."""
     import torch
     frames = []
     for i in range(11):
@@ -166,7 +139,7 @@ def test_fixed_hot_list_in_batched_gathers(monkeypatch):
         ref.check(ref.lib.rrte_hip_render(ref.h, sc.ref(), C.byref(prm), buf.ctypes.data_as(C.POINTER(C.c_uint8))))
         want.append(buf)
     ref.close()
-    ctx = _ctx(monkeypatch, "2", abi.JIT_ON, RRTE_FORCE_GATHER="1", RRTE_TILE_SPLIT="1")
+    ctx = _ctx(monkeypatch, "2", abi.JIT_ON, RRTE_FORCE_GATHER="1")
     lib = ctx.lib
     uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
     ctx.check(lib.rrte_hip_comm_unique_id(uid))
@@ -180,28 +153,97 @@ def test_fixed_hot_list_in_batched_gathers(monkeypatch):
                                                     C.c_void_p(streams[i % 2].cuda_stream)))
     ctx.check(lib.rrte_hip_flush(ctx.h))
     ctx.check(lib.rrte_hip_synchronize(ctx.h))
-    assert ctx.stats().hot_tiles == _fixed_slots(40 * 25, 3)  # per launch: split tiles x 3 parts + whole tiles
+    assert ctx.stats().hot_tiles == 40 * 25
     for i, o in enumerate(outs):
         got = o.cpu().numpy().view(np.uint8)
         assert np.array_equal(got, want[i]), f"frame {i}: {(got != want[i]).sum()} bytes differ"
     ctx.close()
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_measured_lpt_order(split, monkeypatch):
-    """RRTE_TILE_ORDER=3: after the profile every tile of the frame is dispatched in measured-cost
-    order (no image-order rows), the slowest ones optionally split; identical to image order."""
-    objs, lights, cam, cfg = scenes.sdf_showcase(480, 272)
+def test_list_versions_recycle_in_flight(monkeypatch):
+    """RRTE_TEST_RECYCLE=1: a new tile-list version per launch, so the pool of 16 versions wraps
+    while frames are in flight on 4 streams; a version is only reused after the launches that read
+    it have completed (no device synchronisation), and every frame stays exact."""
+    import torch
+    objs, lights, cam, cfg = scenes.sdf_showcase(320, 200)
     sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
     ref = _ctx(monkeypatch, "0", abi.JIT_ON)
     want = _render(ref, sc, prm)
     ref.close()
-    ctx = _ctx(monkeypatch, "3", abi.JIT_ON, RRTE_TILE_SPLIT=split)
-    tiles = 60 * 34
-    seen = 0
-    for _ in range(5):
-        got = _render(ctx, sc, prm)
-        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[2]
-        seen = max(seen, got[3])
-    assert seen >= tiles  # every tile has a slot (split parts add more)
+    ctx = _ctx(monkeypatch, "2", abi.JIT_ON, RRTE_TEST_RECYCLE="1")
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    outs = [torch.full((320 * 200,), -1, dtype=torch.int32, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()
+    n = 40
+    for i in range(n):
+        ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), outs[i % 4].data_ptr(), None,
+                                                C.c_void_p(streams[i % 4].cuda_stream)))
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    assert ctx.stats().hot_tiles == 40 * 25
+    assert int(ctx.stats().shadow_rays) == n * int(want[2])
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint8), want[0])
+    ctx.close()
+
+
+def _threads():
+    return int(os.environ.get("RRTE_ORACLE_THREADS", min(16, os.cpu_count() or 1)))
+
+
+@pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160)])
+def test_timed_configuration_matches_oracle(w, h, monkeypatch):
+    """the bench's own configuration -- default tile policy, 4 frames in flight on 4
+    streams, scene-specialised kernel, RGBA8 frames -- run until the measured whole-frame order has
+    landed (hot_tiles == tiles); then the last frames in flight are compared byte for byte with the
+    ORACLE's frame and the shadow-ray count of every frame with the oracle's, and the same policy's
+    linear floats bit for bit with the oracle's linear image."""
+    import torch
+    objs, lights, cam, cfg = scenes.sdf_showcase(w, h)
+    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    want8, _, want_shadow = oracle.render(sc, prm, nthreads=_threads(), want_f32=False)
+    _, want_lin, _ = oracle.render(sc, prm, nthreads=_threads(), linear=True)
+    ctx = _ctx(monkeypatch, None, abi.JIT_ON)
+    F = 4
+    streams = [torch.cuda.Stream() for _ in range(F)]
+    outs = [torch.full((w * h,), -1, dtype=torch.int32, device="cuda") for _ in range(F)]
+    torch.cuda.synchronize()
+    tiles = ((w + 7) // 8) * ((h + 7) // 8)
+    go = lambda i: ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), outs[i % F].data_ptr(),  # noqa: E731
+                                                           None, C.c_void_p(streams[i % F].cuda_stream)))
+    landed, i = False, 0
+    for _ in range(40):  # rounds of F frames until the profile's list is in use
+        for _ in range(F):
+            go(i)
+            i += 1
+        landed = ctx.stats().hot_tiles == tiles
+        if landed:
+            break
+        ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    assert landed, "the measured tile order never landed"
+    for _ in range(2 * F):  # frames in flight on the measured order
+        go(i)
+        i += 1
+    assert ctx.stats().hot_tiles == tiles
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    assert int(ctx.stats().shadow_rays) == 3 * F * want_shadow  # the landing round + 2 rounds, since the last sync
+    for o in outs:
+        got = o.cpu().numpy().view(np.uint8)
+        d = np.abs(got.astype(np.int16) - want8.astype(np.int16))
+        assert d.max() <= 1, f"u8 max diff {d.max()}"
+        assert (d != 0).sum() <= 16, f"{int((d != 0).sum())} bytes differ (gamma powf ulps only)"
+    # linear floats of the same policy (f32 output: the powf gamma path), frames in flight
+    p = abi.RenderParams.from_buffer_copy(prm)
+    p.flags |= abi.FLAG_F32_LINEAR
+    f32s = [torch.zeros(w * h * 4, dtype=torch.float32, device="cuda") for _ in range(F)]
+    torch.cuda.synchronize()
+    for j in range(2 * F):
+        ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(p), None, f32s[j % F].data_ptr(),
+                                                C.c_void_p(streams[j % F].cuda_stream)))
+    assert ctx.stats().hot_tiles == tiles
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    assert int(ctx.stats().shadow_rays) == 2 * F * want_shadow
+    for f in f32s:
+        got = f.cpu().numpy().view(np.uint32)
+        bad = (got != want_lin.view(np.uint32)).reshape(-1, 4).any(-1)
+        assert not bad.any(), f"{int(bad.sum())} pixels differ from the oracle's linear image"
     ctx.close()

@@ -1,5 +1,5 @@
-"""The Rust `-sys` binding in INTEGRATION.md §1, checked mechanically against include/rrte_hip.h
-(VERDICT r02 #9).  There is no cargo here, so the block cannot be compiled; instead:
+"""The Rust crates under rust/ (rrte-hip-sys, rrte-renderer-hip) and the reference patches, checked
+mechanically.  There is no cargo here, so they cannot be compiled; instead:
 
 * every `#[repr(C)]` struct: field names and order equal the header's, and the repr(C) layout the
   Rust types imply (offsets, size) equals offsetof/sizeof from a C program compiled with the header;
@@ -12,6 +12,7 @@ The real caller this protects is crates/rrte-renderer/src/raytracer.rs:35-51 via
 crates/rrte-core/src/engine.rs:280-312 (a struct-layout drift would corrupt every frame silently)."""
 import re
 import subprocess
+import sys
 from pathlib import Path
 
 import pytest
@@ -20,12 +21,12 @@ ROOT = Path(__file__).resolve().parents[1]
 HEADER = ROOT / "include" / "rrte_hip.h"
 
 
+SYS_LIB = ROOT / "rust" / "rrte-hip-sys" / "src" / "lib.rs"
+
+
 def _rust_block():
-    text = (ROOT / "INTEGRATION.md").read_text()
-    blocks = re.findall(r"```rust\n(.*?)```", text, re.S)
-    lib = [b for b in blocks if "crates/rrte-hip-sys/src/lib.rs" in b]
-    assert len(lib) == 1, "INTEGRATION.md must hold exactly one rrte-hip-sys lib.rs block"
-    return re.sub(r"//[^\n]*", "", lib[0])
+    """rust/rrte-hip-sys/src/lib.rs without comments (the crate's FFI declarations)."""
+    return re.sub(r"//[^\n]*", "", SYS_LIB.read_text())
 
 
 def _split_top(s):
@@ -254,3 +255,234 @@ def test_checker_catches_a_layout_drift(mutate, tmp_path):
         lay = rust_layout({"rrte_render_params": fields})
         c = c_offsets({"rrte_render_params": fields}, tmp_path)
         assert lay["rrte_render_params"][0] != c["rrte_render_params"]
+
+
+# ------------------------------------------------------------------ the lowering
+CPP = ROOT / "rrte_amd" / "cpp" / "rrte_renderer.cpp"
+LOWER_RS = ROOT / "rust" / "rrte-renderer-hip" / "src" / "lower.rs"
+SDF_RS = ROOT / "rust" / "rrte-renderer-hip" / "src" / "sdf.rs"
+
+
+def _strip_comments(t):
+    return re.sub(r"//[^\n]*", "", t)
+
+
+def _norm(tok):
+    """One argument, language-neutral: no casts, derefs, self., member underscores, f suffixes."""
+    t = " ".join(tok.split())
+    t = re.sub(r"\(float\)|\(double\)|\(uint32_t\)", "", t)
+    t = re.sub(r"\s+as\s+(f32|f64|u32|i32)\b", "", t)
+    t = t.replace("rrte_math::ZERO", "ZERO").replace("*", "").replace("self.", "").replace("?", "")
+    t = re.sub(r"\b(\w+)_\b", r"\1", t)                     # albedo_ -> albedo (C++ member names)
+    t = re.sub(r"(\d+\.\d*(?:e-?\d+)?)f\b", r"\1", t)      # 0.0f -> 0.0
+    return t.replace(" ", "")
+
+
+def _args(s):
+    return [_norm(a) for a in _split_top(s)]
+
+
+def _cpp_calls(fn_name_re, callee, text):
+    """{kind constant: [args]} of `callee(KIND, ...)` inside C++ functions whose name matches."""
+    out = {}
+    for m in re.finditer(r"(\w+)::lower\([^)]*\) const \{", text):
+        if not re.match(fn_name_re, m.group(1)):
+            continue
+        body = " ".join(text[m.end():m.end() + 400].split())  # the function's first call
+        c = re.search(callee + r"\((RRTE_\w+),\s*(.*?)\);", body)
+        if c:
+            out[c.group(1)] = c.group(2)
+    return out
+
+
+def _braced(s):
+    """`{a, b}` (C++ init list) or `&[a, b]` (Rust slice) -> inner text."""
+    s = s.strip()
+    m = re.match(r"&?[\[{](.*)[\]}]$", s, re.S)
+    return m.group(1) if m else s
+
+
+def test_prim_lowering_matches_the_cpp_mirror():
+    """Every SceneObject: the same kind constant and the same p[] values in the same order as the
+    C++ mirror's `X::lower` (which the GPU suite renders against the oracle)."""
+    cpp = _strip_comments(CPP.read_text())
+    want = {}
+    for cls in ("Sphere", "Plane", "Triangle", "Cube", "Cylinder", "Cone", "Capsule"):
+        m = re.search(cls + r"::lower\(Lowering&\) const \{(.*?)\n\}", cpp, re.S)
+        body = " ".join(m.group(1).split())
+        c = re.search(r"prim\((RRTE_PRIM_\w+),\s*\{(.*?)\}\)", body)
+        want[c.group(1)] = _args(c.group(2))
+    rs = " ".join(_strip_comments(LOWER_RS.read_text()).split())
+    got = {}
+    for kind, args in re.findall(r"prim\(\s*(RRTE_PRIM_(?:SPHERE|PLANE|TRIANGLE|CUBE|CYLINDER|CONE|CAPSULE)),\s*&\[(.*?)\],\s*t,?\s*\)", rs):
+        got[kind] = _args(args)
+    assert set(got) == set(want), (set(want) - set(got), set(got) - set(want))
+    for kind in want:
+        assert got[kind] == want[kind], (kind, got[kind], want[kind])
+    # the transform columns: same fields in the same order
+    c_trs = re.search(r"fill\(r\.trs, \{(.*?)\}\);", " ".join(cpp.split())).group(1)
+    r_trs = re.search(r"r\.trs = \[(.*?)\];", rs).group(1)
+    assert _args(c_trs) == _args(r_trs)
+
+
+def test_sdf_object_lowering_matches_the_cpp_mirror():
+    """SDFObject: the bound inflation and every march field the C++ lowering assigns."""
+    cpp = " ".join(_strip_comments(CPP.read_text()).split())
+    sdf = " ".join(_strip_comments(SDF_RS.read_text()).split())
+    rs = " ".join(_strip_comments(LOWER_RS.read_text()).split())
+    assert "const double r = b.r * 1.001 + 1e-3;" in cpp and "let r = b.r * 1.001 + 1e-3;" in sdf
+    body = re.search(r"rrte_prim SDFObject::lower\(Lowering& lw\) const \{(.*?)return p; \}", cpp).group(1)
+    cf = set(re.findall(r"\bp\.(sdf_\w+) =", body))
+    rf = set(re.findall(r"\bp\.(sdf_\w+) =", rs))
+    assert cf == rf == {"sdf_first", "sdf_count", "sdf_max_steps", "sdf_step_scale", "sdf_hit_eps"}
+    assert "RRTE_PRIM_SDF" in rs
+    # default march parameters and the deformer step scale
+    assert "128, None, 1e-4" in sdf and "if sdf.has_deformer() { 0.6 } else { 1.0 }" in sdf
+    assert "sdf->has_deformer() ? 0.6f : 1.0f" in cpp
+
+
+def _cpp_defaults(cpp, fn):
+    """Default arguments of a C++ helper signature: [(name, default or None)]."""
+    sig = re.search(fn + r"\((.*?)\)\s*\{", " ".join(cpp.split())).group(1)
+    out = []
+    for a in _split_top(sig):
+        name = a.split("=")[0].split()[-1]
+        out.append((name, _norm(a.split("=", 1)[1]) if "=" in a else None))
+    return out
+
+
+def test_light_and_material_lowering_match_the_cpp_mirror():
+    cpp = _strip_comments(CPP.read_text())
+    rs = " ".join(_strip_comments(LOWER_RS.read_text()).split())
+    lights = _cpp_calls(r".*Light$", "light_struct", cpp)
+    defaults = _cpp_defaults(cpp, "rrte_light light_struct")
+    got = dict(re.findall(r"light_struct\(\s*(RRTE_LIGHT_\w+),\s*(.*?)\)\s*(?:,\s*GpuLight|\}|$)", rs))
+    assert set(lights) == set(got) == {"RRTE_LIGHT_POINT", "RRTE_LIGHT_DIRECTIONAL", "RRTE_LIGHT_SPOT",
+                                       "RRTE_LIGHT_AMBIENT"}
+    for kind, args in lights.items():
+        a = _args(args)
+        a += [d for _, d in defaults[1 + len(a):]]  # the C++ call's omitted arguments: their defaults
+        assert _args(got[kind]) == a, (kind, _args(got[kind]), a)
+    mats = _cpp_calls(r".*Material$", "material_struct", cpp)
+    mgot = dict(re.findall(r"material_struct\((RRTE_MAT_\w+),\s*([^)]*)\)", rs))
+    assert set(mats) == set(mgot) == {"RRTE_MAT_LAMBERTIAN", "RRTE_MAT_METAL", "RRTE_MAT_DIELECTRIC",
+                                      "RRTE_MAT_EMISSIVE"}
+    for kind, args in mats.items():
+        assert _args(mgot[kind]) == _args(args), (kind, mgot[kind], args)
+    # the helpers fill the same record fields
+    for helper, var in (("light_struct", "l"), ("material_struct", "m")):
+        cb = re.search(helper + r"\(.*?\)\s*\{(.*?)\n\}", cpp, re.S).group(1)
+        rb = re.search(helper + r"\(.*?\)\s*->\s*\w+\s*\{(.*?)\}", rs).group(1)
+        cf = set(re.findall(r"\b" + var + r"\.(\w+) =", cb)) | set(re.findall(r"fill\(" + var + r"\.(\w+),", cb))
+        rf = set(re.findall(r"\b" + var + r"\.(\w+) =", rb))
+        assert cf == rf, (helper, cf ^ rf)
+
+
+def test_camera_and_config_lowering_match_the_cpp_mirror():
+    cpp = " ".join(_strip_comments(CPP.read_text()).split())
+    rs = " ".join(_strip_comments(LOWER_RS.read_text()).split())
+    cb = re.search(r"rrte_camera Camera::lower\(\) const \{(.*?)return c; \}", cpp).group(1)
+    rb = re.search(r"pub fn lower_camera\(.*?\{(.*?)\bc \}", rs).group(1)
+    cf = set(re.findall(r"\bc\.(\w+) =", cb)) | set(re.findall(r"fill\(c\.(\w+),", cb))
+    rf = set(re.findall(r"\bc\.(\w+) =", rb))
+    assert cf == rf, cf ^ rf
+    cb = re.search(r"rrte_render_params RaytracerConfig::lower\(\) const \{(.*?)return p; \}", cpp).group(1)
+    rb = re.search(r"pub fn lower_config\(.*?\{(.*?)\bp \}", rs).group(1)
+    cf = set(re.findall(r"\bp\.(\w+) =", cb)) | set(re.findall(r"fill\(p\.(\w+),", cb))
+    rf = set(re.findall(r"\bp\.(\w+) =", rb))
+    assert cf == rf, cf ^ rf
+
+
+def _positional(args, params):
+    """Arguments with the function's parameter names replaced by their positions ($0, $1, ...)."""
+    out = []
+    for a in args:
+        for i, n in enumerate(params):
+            a = re.sub(r"\b" + re.escape(n) + r"\b", f"${i}", a)
+        out.append(a)
+    return out
+
+
+def test_sdf_builders_match_the_cpp_mirror():
+    """The build-defined SDF surface (README.md:303-328, 496-510): every leaf builder emits the same
+    node op and parameters, every deformer the same op, floats and integer arguments (parameters
+    compared by position: the Rust names follow Rust conventions)."""
+    cpp = " ".join(_strip_comments(CPP.read_text()).split())
+    rs = " ".join(_strip_comments(SDF_RS.read_text()).split())
+
+    def cparams(sig):
+        return [a.split()[-1] for a in _split_top(sig)]
+
+    def rparams(sig):
+        return [a.split(":")[0].strip() for a in _split_top(sig)]
+
+    leaves = ("sphere", "box", "cylinder", "prism", "torus", "tube", "ring", "cone", "capsule", "ellipsoid")
+    for name in leaves:
+        c = re.search(r"SDFRef sdf_" + name + r"\((.*?)\) \{.*?make_shared<Leaf>\((RRTE_SDF_\w+), c, std::vector<float>\{(.*?)\},", cpp)
+        r = re.search(r"pub fn sdf_" + name + r"\((.*?)\) -> SdfRef \{.*?Leaf \{ op: (RRTE_SDF_\w+), c, f: vec!\[(.*?)\],", rs)
+        assert c and r, name
+        assert c.group(2) == r.group(2), name
+        a, b = _positional(_args(c.group(3)), cparams(c.group(1))), _positional(_args(r.group(3)), rparams(r.group(1)))
+        assert a == b, (name, a, b)
+    for name in ("twist", "bend", "taper", "noise", "wave"):
+        c = re.search(r"DeformerRef " + name + r"\((.*?)\) \{.*?node\((RRTE_SDF_\w+), \{(.*?)\}, \{(.*?)\}\)", cpp)
+        r = re.search(r"pub fn " + name + r"\((.*?)\)\s*-> Result<DeformerRef, SdfError> \{.*?node\((RRTE_SDF_\w+), &\[(.*?)\], &\[(.*?)\]\)", rs)
+        assert c and r, name
+        assert c.group(2) == r.group(2), name
+        cp, rp = cparams(c.group(1)), rparams(r.group(1))
+        for k in (3, 4):
+            a, b = _positional(_args(c.group(k)), cp), _positional(_args(r.group(k)), rp)
+            assert a == b, (name, a, b)
+
+
+# ------------------------------------------------------------ the reference patches (VERDICT r03 #4)
+PATCHES = ROOT / "rust" / "patches"
+REFERENCE = Path("/root/reference")
+
+
+def test_patches_hook_every_reference_type():
+    p1 = (PATCHES / "0001-rrte-renderer-gpu-desc.patch").read_text()
+    for cls in ("Sphere", "Plane", "Triangle", "Cube", "Cylinder", "Cone", "Capsule"):
+        assert re.search(r"impl SceneObject for " + cls + r" \{\n\+    fn gpu_desc", p1), cls
+    for cls in ("DirectionalLight", "PointLight", "SpotLight", "AmbientLight"):
+        assert re.search(r"impl Light for " + cls + r" \{\n\+    fn gpu_desc", p1), cls
+    for cls in ("LambertianMaterial", "MetalMaterial", "DielectricMaterial", "EmissiveMaterial"):
+        assert re.search(r"impl Material for " + cls + r" \{\n\+    fn gpu_desc", p1), cls
+    assert "+pub trait RenderBackend" in p1 and "+    pub fn set_backend" in p1
+    p2 = (PATCHES / "0002-rrte-core-hip-backend.patch").read_text()
+    assert "+                self.frame_buffer = raytracer.render(self.scene.get_objects(), self.scene.get_lights()," in p2
+    assert "rrte_renderer_hip::HipBackend::new" in p2
+
+
+@pytest.mark.skipif(not REFERENCE.exists(), reason="the reference checkout is not on this machine")
+def test_patches_apply_and_are_current(tmp_path):
+    """The committed patches apply to the reference snapshot and equal what tools/make_rust_patches.py
+    generates from it."""
+    import shutil
+    work = tmp_path / "ref"
+    work.mkdir()
+    shutil.copy(REFERENCE / "Cargo.toml", work / "Cargo.toml")
+    shutil.copytree(REFERENCE / "crates", work / "crates")
+    for p in sorted(PATCHES.glob("*.patch")):
+        r = subprocess.run(["patch", "-p1", "--forward", "-i", str(p)], cwd=work, capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+    assert (work / "crates/rrte-renderer/src/gpu_desc.rs").exists()
+    gen = tmp_path / "gen"
+    env = dict(__import__("os").environ, RRTE_REFERENCE=str(REFERENCE))
+    code = (f"import sys; sys.path.insert(0, {str(ROOT / 'tools')!r}); import make_rust_patches as m; "
+            f"from pathlib import Path; m.OUT = Path({str(gen)!r}); m.main()")
+    subprocess.run([sys.executable, "-c", code], check=True, env=env, capture_output=True)
+    for p in sorted(PATCHES.glob("*.patch")):
+        assert (gen / p.name).read_text() == p.read_text(), f"{p.name} is stale: rerun tools/make_rust_patches.py"
+
+
+def test_lowering_checker_catches_a_swapped_argument(monkeypatch, tmp_path):
+    """The checker itself: a Rust lowering that swaps a cylinder's radius and height must fail."""
+    bad = LOWER_RS.read_text().replace("prim(RRTE_PRIM_CYLINDER, &[center.x, center.y, center.z, *radius, *height], t)",
+                                       "prim(RRTE_PRIM_CYLINDER, &[center.x, center.y, center.z, *height, *radius], t)")
+    assert bad != LOWER_RS.read_text()
+    f = tmp_path / "lower.rs"
+    f.write_text(bad)
+    monkeypatch.setattr(sys.modules[__name__], "LOWER_RS", f)
+    with pytest.raises(AssertionError):
+        test_prim_lowering_matches_the_cpp_mirror()

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 profiles of the headline on one GPU, outputs under gpurun_out/prof_<tag>/:
+# Profiles of the headline on one GPU, outputs under gpurun_out/prof_<tag>/:
 #  trace/  rocprofv3 --kernel-trace --stats of frames launched one after another (--inflight 1): the
 #          per-launch kernel duration bench.py's roofline.avg_launch_ms is compared with;
 #  tl/     the kernel trace of the driver's configuration (20 timed steps, 5 warm-up, 4 in flight):
