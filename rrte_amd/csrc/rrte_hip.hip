@@ -43,6 +43,7 @@ struct LaunchPlan {
     bool cull, single;
     uint32_t num_prims, num_lights, num_materials;
     uint32_t gx, gy;
+    int prof = 0;  // tile-profile slot (rrte_ctx::tprof): 0 whole frames / rank shares, 1 + i chunk i of a blocking frame
 };
 
 // A tile order composed off the render thread (plan_tile_order): the profile's shape key and the
@@ -255,7 +256,18 @@ struct rrte_ctx {
         uint64_t cam_sig = 0;            // camera of the last profiled launch (frame 0's FrameCam)
         std::future<TilePlanResult> work;  // composition of the last profile's order (worker thread)
         bool working = false;
-    } tprof;
+    };
+    // One tile-order state per launch shape that alternates within a frame: slot 0 for whole frames
+    // and rank shares, slot 1 + i for row chunk i of a blocking frame (render_chunked)
+    static constexpr int kBndChunksMax = 8, kProfSlots = 1 + kBndChunksMax;
+    TileProfile tprof[kProfSlots];
+    // Blocking drop-in path (rrte_hip_render into a host buffer): the frame renders as row chunks on
+    // streams of their own, and each chunk's D2H starts as soon as that chunk is done (render_chunked)
+    int bnd_chunks = 4;                       // RRTE_BND_CHUNKS (1: one launch, then one copy)
+    hipStream_t bnd_stream[kBndChunksMax] = {};
+    hipStream_t bnd_copy = nullptr;
+    hipEvent_t ev_bchunk[kBndChunksMax] = {};
+    hipEvent_t ev_bcopy = nullptr;
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed scrambled permutation of the tiles (tests)
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
@@ -1102,9 +1114,10 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
 }
 
 LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
-                       uint32_t internal_flags) {
+                       uint32_t internal_flags, uint32_t row0 = 0u) {
     LaunchPlan L;
     L.k = make_params(c, s, p, rows);
+    L.k.row0 = row0;  // (image rows [row0, row0 + rows); band_rows == 0)
     L.k.flags |= internal_flags;
     L.mode = (int)p->mode;
     L.cull = cull_policy(s, p->mode, c->env_cull);
@@ -1171,8 +1184,7 @@ std::vector<uint32_t> fixed_slots(uint32_t n, uint32_t tiles_x) {
 // Allocates what an upload of up to `words` list words needs -- pinned staging, the upload stream and
 // the device versions not yet allocated -- at profile time, so the first upload (inside a later render
 // call) allocates nothing.
-bool reserve_hot_lists(rrte_ctx* c, size_t words) {
-    auto& tp = c->tprof;
+bool reserve_hot_lists(rrte_ctx::TileProfile& tp, size_t words) {
     if (tp.cap_h_list < words) {
         if (tp.h_list) (void)hipHostFree(tp.h_list);  // (pinned staging: every copy from it was synchronised)
         tp.h_list = nullptr;
@@ -1195,8 +1207,7 @@ bool reserve_hot_lists(rrte_ctx* c, size_t words) {
 // first; a version is free once every launch that read it has completed (struct Retire).  The copy
 // runs on the list's own upload stream and is synchronised (it holds nothing else), so every launch
 // sees a whole list.
-bool upload_hot_list(rrte_ctx* c) {
-    auto& tp = c->tprof;
+bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
     constexpr int K = rrte_ctx::TileProfile::kVersions;
     int pick = -1;
     for (int k = 1; k <= K && pick < 0; ++k) {  // the oldest retired version first
@@ -1214,7 +1225,7 @@ bool upload_hot_list(rrte_ctx* c) {
         if (hipMalloc(reinterpret_cast<void**>(&tp.d_list[pick]), bytes) != hipSuccess) return false;
         tp.cap_list[pick] = words;
     }
-    if (!reserve_hot_lists(c, words)) return false;
+    if (!reserve_hot_lists(tp, words)) return false;
     memcpy(tp.h_list, tp.slots.data(), bytes);
     if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
         hipStreamSynchronize(tp.upload_stream) != hipSuccess)
@@ -1236,7 +1247,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     // (RRTE_DEBUG bit 5 runs one workgroup in image-order numbering: no tile order; bit 4's per-wave
     // stamps work with it)
     if (!c->env_tile_order || c->env_wg256 || L.gx > 0xffffu || L.gy > 0xffffu || (k.debug & 32u)) return false;
-    auto& tp = c->tprof;
+    auto& tp = c->tprof[L.prof];
     std::string key(reinterpret_cast<const char*>(&kern), sizeof kern);
     const uint32_t shape[] = {k.width, k.height, k.rows, k.row0, k.band_rows, k.nranks, k.rank, k.spp, k.max_depth,
                               (uint32_t)L.mode, (uint32_t)L.cull, (uint32_t)L.single};
@@ -1290,7 +1301,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         if (retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
         tp.cur = -1;
     }
-    if (!tp.slots.empty() && tp.slots.size() == tiles && (tp.cur >= 0 || upload_hot_list(c))) {
+    if (!tp.slots.empty() && tp.slots.size() == tiles && (tp.cur >= 0 || upload_hot_list(c, tp))) {
         k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
         tp.ret[tp.cur].use(st);
@@ -1306,7 +1317,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         tp.cap_h = tiles;
     }
     if (!tp.ev && hipEventCreateWithFlags(&tp.ev, hipEventDisableTiming) != hipSuccess) return false;
-    if (!reserve_hot_lists(c, tiles)) return false;
+    if (!reserve_hot_lists(tp, tiles)) return false;
     k.tile_cost = tp.d_cost;  // every tile of frame 0 stores its duration (no clearing needed)
     tp.cam_sig = cam;
     tp.pending_key = key;
@@ -1316,8 +1327,8 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
 }
 
 // Queues the profiled launch's copy-back on its stream (plan_tile_order returned true).
-rrte_status finish_tile_order(rrte_ctx* c, bool profile, hipStream_t st) {
-    auto& tp = c->tprof;
+rrte_status finish_tile_order(rrte_ctx* c, const LaunchPlan& L, bool profile, hipStream_t st) {
+    auto& tp = c->tprof[L.prof];
     if (!profile) return RRTE_OK;
     HIPCHK(c, hipMemcpyAsync(tp.h_cost, tp.d_cost, (size_t)tp.tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipEventRecord(tp.ev, st));
@@ -1349,7 +1360,7 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         else
             HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, st, args, nullptr));
         hs.lap(8);
-        return finish_tile_order(c, profile, st);
+        return finish_tile_order(c, L, profile, st);
     }
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
                  c->mesh_view};
@@ -1361,13 +1372,15 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     else
         hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     HIPCHK(c, hipGetLastError());
-    return finish_tile_order(c, profile, st);
+    return finish_tile_order(c, L, profile, st);
 }
 
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
-                   uint32_t* d_rgba, float4* d_f32, hipStream_t st, uint32_t internal_flags = 0u) {
+                   uint32_t* d_rgba, float4* d_f32, hipStream_t st, uint32_t internal_flags = 0u, uint32_t row0 = 0u,
+                   int prof = 0) {
     if (rows == 0) return RRTE_OK;
-    LaunchPlan L = plan_launch(c, s, p, rows, internal_flags);
+    LaunchPlan L = plan_launch(c, s, p, rows, internal_flags, row0);
+    L.prof = prof;
     return issue_launch(c, L, d_rgba, d_f32, st);
 }
 
@@ -1388,6 +1401,46 @@ rrte_status finish_frame(rrte_ctx* c) {
     return RRTE_OK;
 }
 
+// The blocking drop-in path into a host RGBA8 buffer (Raytracer::render, raytracer.rs:45-89): the
+// frame renders as `n` row chunks (multiples of 16 rows, so camera-culling tiles never straddle two
+// chunks), each launched on a stream of its own so they run together as one frame would, each in its
+// own measured-cost tile order (tile-profile slot 1 + i).  Each chunk's D2H copy starts on the copy
+// stream as soon as that chunk's kernel has completed -- the kernel boundary orders its stores, no
+// fences -- so the 8.3 MB PCIe copy (~150 us at ~55 GB/s) overlaps the rest of the render instead of
+// following all of it.  Copies run top to bottom.
+rrte_status render_chunked(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out8,
+                           uint32_t n) {
+    const uint32_t W = p->width, H = p->height;
+    const uint32_t rows = (((H + n - 1) / n) + 15u) & ~15u;
+    n = (H + rows - 1) / rows;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!c->bnd_stream[i]) HIPCHK(c, hipStreamCreateWithFlags(&c->bnd_stream[i], hipStreamNonBlocking));
+        if (!c->ev_bchunk[i]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_bchunk[i], hipEventDisableTiming));
+    }
+    if (!c->bnd_copy) HIPCHK(c, hipStreamCreateWithFlags(&c->bnd_copy, hipStreamNonBlocking));
+    if (!c->ev_bcopy) HIPCHK(c, hipEventCreateWithFlags(&c->ev_bcopy, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));  // after the work already queued on the context's stream
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t r0 = i * rows, nr = std::min(rows, H - r0);
+        HIPCHK(c, hipStreamWaitEvent(c->bnd_stream[i], c->ev0, 0));
+        rrte_status r = launch(c, s, p, nr, c->d_rgba + (size_t)r0 * W, nullptr, c->bnd_stream[i], 0u, r0, 1 + (int)i);
+        if (r != RRTE_OK) return r;
+        HIPCHK(c, hipEventRecord(c->ev_bchunk[i], c->bnd_stream[i]));
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t r0 = i * rows, nr = std::min(rows, H - r0);
+        HIPCHK(c, hipStreamWaitEvent(c->bnd_copy, c->ev_bchunk[i], 0));
+        HIPCHK(c, hipMemcpyAsync(out8 + (size_t)r0 * W * 4, c->d_rgba + (size_t)r0 * W, (size_t)nr * W * 4,
+                                 hipMemcpyDeviceToHost, c->bnd_copy));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_bcopy, c->bnd_copy));
+    // the context's stream: every chunk (ev1: the render's end, rrte_stats.kernel_ms), then the copies
+    for (uint32_t i = 0; i < n; ++i) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bchunk[i], 0));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bcopy, 0));
+    return RRTE_OK;
+}
+
 rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out8,
                           float* outf) {
     rrte_status r = validate(c, s, p);
@@ -1402,17 +1455,22 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     const int nr = c->nranks, rk = c->rank;
     c->nranks = 1;
     c->rank = 0;
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    r = launch(c, s, p, p->height, c->d_rgba, outf ? c->d_f32 : nullptr, c->stream);
+    const bool chunked = out8 && !outf && c->bnd_chunks > 1 && p->height >= 32u && !c->env_debug;
+    if (chunked) {
+        r = render_chunked(c, s, p, out8, (uint32_t)c->bnd_chunks);
+    } else {
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        r = launch(c, s, p, p->height, c->d_rgba, outf ? c->d_f32 : nullptr, c->stream);
+        if (r == RRTE_OK) r = hipEventRecord(c->ev1, c->stream) == hipSuccess ? RRTE_OK : RRTE_HIP_ERROR;
+    }
     c->nranks = nr;
     c->rank = rk;
     if (r != RRTE_OK) return r;
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->pending_kernel_timing = true;
     c->pending_primary = (uint64_t)npix * p->samples_per_pixel;
     c->stats.upload_ms = up;
     c->stats.gather_ms = 0.0;
-    if (out8) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
+    if (out8 && !chunked) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
     if (outf) HIPCHK(c, hipMemcpyAsync(outf, c->d_f32, npix * 16, hipMemcpyDeviceToHost, c->stream));
     if ((r = finish_frame(c)) != RRTE_OK) return r;
     c->stats.frames++;
@@ -1489,6 +1547,8 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         c->env_tile_order_fixed = g[0] == '2';  // 0 image order, 2 fixed permutation (tests), else measured (default)
     }
     if (const char* g = getenv("RRTE_TEST_RECYCLE")) c->env_test_recycle = g[0] == '1';
+    if (const char* g = getenv("RRTE_BND_CHUNKS"); g && *g)
+        c->bnd_chunks = std::max(1, std::min(rrte_ctx::kBndChunksMax, (int)strtol(g, nullptr, 0)));
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
@@ -1556,15 +1616,24 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_stall) (void)hipHostFree(c->h_stall);
-    if (c->tprof.d_cost) (void)hipFree(c->tprof.d_cost);
-    if (c->tprof.h_cost) (void)hipHostFree(c->tprof.h_cost);
-    if (c->tprof.ev) (void)hipEventDestroy(c->tprof.ev);
-    for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i) {
-        if (c->tprof.d_list[i]) (void)hipFree(c->tprof.d_list[i]);
-        destroy_events(c->tprof.ret[i]);
+    for (auto& tp : c->tprof) {
+        if (tp.working) tp.work.wait();
+        if (tp.d_cost) (void)hipFree(tp.d_cost);
+        if (tp.h_cost) (void)hipHostFree(tp.h_cost);
+        if (tp.ev) (void)hipEventDestroy(tp.ev);
+        for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i) {
+            if (tp.d_list[i]) (void)hipFree(tp.d_list[i]);
+            destroy_events(tp.ret[i]);
+        }
+        if (tp.h_list) (void)hipHostFree(tp.h_list);
+        if (tp.upload_stream) (void)hipStreamDestroy(tp.upload_stream);
     }
-    if (c->tprof.h_list) (void)hipHostFree(c->tprof.h_list);
-    if (c->tprof.upload_stream) (void)hipStreamDestroy(c->tprof.upload_stream);
+    for (int i = 0; i < rrte_ctx::kBndChunksMax; ++i) {
+        if (c->bnd_stream[i]) (void)hipStreamDestroy(c->bnd_stream[i]);
+        if (c->ev_bchunk[i]) (void)hipEventDestroy(c->ev_bchunk[i]);
+    }
+    if (c->bnd_copy) (void)hipStreamDestroy(c->bnd_copy);
+    if (c->ev_bcopy) (void)hipEventDestroy(c->ev_bcopy);
     if (c->upload_stream) (void)hipStreamDestroy(c->upload_stream);
     for (hipEvent_t e : c->ev_poll)
         if (e) (void)hipEventDestroy(e);

@@ -59,3 +59,31 @@ def test_blocking_render_generic_kernel_and_size_changes():
         assert np.abs(got.astype(int) - r8.astype(int)).max() <= 1, (w, h)
         assert int(ctx.stats().shadow_rays) == rsh
     ctx.close()
+
+
+@pytest.mark.parametrize("chunks", ["1", "3", "8"])
+@pytest.mark.parametrize("w,h", [(1920, 1080), (333, 97), (200, 40)])
+def test_chunked_blocking_render_is_exact(chunks, w, h, monkeypatch):
+    """rrte_hip_render renders row chunks on their own streams, each chunk's D2H starting when the
+    chunk is done (RRTE_BND_CHUNKS; rrte_hip.hip render_chunked): every chunk count, sizes whose
+    chunks end mid-tile or leave a short last chunk, and enough frames for each chunk's measured tile
+    order to land (its own profile slot) -- always the device path's bytes and shadow-ray count."""
+    import torch
+    objs, lights, cam, cfg = scenes.sdf_showcase(w, h)
+    sc = LoweredScene(objs, lights, cam)
+    prm = cfg.lower()
+    ref = Context(0, jit=abi.JIT_ON)
+    dev = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ref.check(ref.lib.rrte_hip_render_async(ref.h, sc.ref(), C.byref(prm), dev.data_ptr(), None, None))
+    ref.check(ref.lib.rrte_hip_synchronize(ref.h))
+    want, want_shadow = dev.cpu().numpy().view(np.uint8), int(ref.stats().shadow_rays)
+    ref.close()
+    monkeypatch.setenv("RRTE_BND_CHUNKS", chunks)
+    ctx = Context(0, jit=abi.JIT_ON)
+    buf = np.full(w * h * 4, 7, np.uint8)
+    for f in range(6):
+        got = _blocking(ctx, sc, prm, buf)
+        assert np.array_equal(got, want), f"frame {f}: {int((got != want).sum())} bytes differ"
+        assert int(ctx.stats().shadow_rays) == want_shadow
+    ctx.close()
