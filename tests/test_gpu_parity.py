@@ -204,7 +204,9 @@ def test_jit_auto_policy_specialises_in_the_background():
         if rt.stats().jit_active:
             break
         assert time.time() - t0 < 120, "the background compile never landed"
-    assert frames >= 3 and rt.stats().jit_compile_ms > 0  # frame 2 only started the compile
+    # frame 1 ran on the generic kernel; frame 2 started the compile -- with the persistent code-object
+    # cache warm it can land within frame 2 itself (a later row chunk of the blocking frame)
+    assert frames >= 2 and rt.stats().jit_compile_ms > 0
     cam.transform.position = (cam.transform.position[0], cam.transform.position[1] + np.float32(0.5),
                               cam.transform.position[2])
     c = rt.render(objs, lights, [], cam)  # camera motion: no recompile, still specialised
