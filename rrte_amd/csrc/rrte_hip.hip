@@ -263,7 +263,10 @@ struct rrte_ctx {
     TileProfile tprof[kProfSlots];
     // Blocking drop-in path (rrte_hip_render into a host buffer): the frame renders as row chunks on
     // streams of their own, and each chunk's D2H starts as soon as that chunk is done (render_chunked)
-    int bnd_chunks = 4;                       // RRTE_BND_CHUNKS (1: one launch, then one copy)
+    // RRTE_BND_CHUNKS (default 1: one launch, then one copy).  Measured slower so far:
+    // every chunk holding object rows is bound by its own slowest tile (~100 us), and the chunks'
+    // launches start 7-17 us apart, so the copies cannot start before ~140 us
+    int bnd_chunks = 1;
     hipStream_t bnd_stream[kBndChunksMax] = {};
     hipStream_t bnd_copy = nullptr;
     hipEvent_t ev_bchunk[kBndChunksMax] = {};
