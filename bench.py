@@ -188,15 +188,21 @@ def measured_valu_peak():
     return {"fma_add_mul": fma, "cmp_select_max": sel, "source": "profiles/r01_valu_peak.json"}
 
 
-def kernel_variants(scene, prm, fulls, sptrs, dev, rays_per_frame, n=60):
+def kernel_variants(scene, prm, fulls, sptrs, dev, rays_per_frame, anim=None, n=60):
     """Secondary throughput of the headline workload per kernel kind (rank 0, N=1; not the headline):
     the generic kernel, the TOPOLOGY specialisation (structure compiled in, values read from the
-    uploaded scene: one compile serves every frame of an animation) and the FULL specialisation (the
-    headline's kernel), each on a context of its own, frames in flight as the headline runs them."""
+    uploaded scene: one compile serves every frame of an animation), the FULL specialisation (the
+    headline's kernel), each on a context of its own, frames in flight as the headline runs them --
+    and `topology_animated`: the topology kernel on an ANIMATION, every frame a new scene (objects,
+    lights and materials changed; rrte_amd.scenes.animate_values), uploaded into the scene-version ring
+    while the earlier frames are in flight (VERDICT r03 #7)."""
     import torch
     out = {}
     F = len(fulls)
-    for kind, jit, topo in (("generic", abi.JIT_OFF, "0"), ("topology", abi.JIT_ON, "1"), ("full", abi.JIT_ON, "0")):
+    kinds = [("generic", abi.JIT_OFF, "0", None), ("topology", abi.JIT_ON, "1", None), ("full", abi.JIT_ON, "0", None)]
+    if anim:
+        kinds.append(("topology_animated", abi.JIT_ON, "1", anim))
+    for kind, jit, topo, frames in kinds:
         old = os.environ.get("RRTE_JIT_TOPO")
         os.environ["RRTE_JIT_TOPO"] = topo  # read at context creation
         try:
@@ -206,23 +212,33 @@ def kernel_variants(scene, prm, fulls, sptrs, dev, rays_per_frame, n=60):
                 os.environ.pop("RRTE_JIT_TOPO", None)
             else:
                 os.environ["RRTE_JIT_TOPO"] = old
-        go = lambda i: c.check(c.lib.rrte_hip_render_async(c.h, scene.ref(), C.byref(prm),  # noqa: E731
+        sc_of = (lambda i: frames[i % len(frames)]) if frames else (lambda i: scene)  # noqa: E731
+        go = lambda i: c.check(c.lib.rrte_hip_render_async(c.h, sc_of(i).ref(), C.byref(prm),  # noqa: E731
                                                            fulls[i % F].data_ptr(), None, sptrs[i % F]))
-        for i in range(F + 1):
+        for i in range(max(F + 1, len(frames) if frames else 0)):
             go(i)
         torch.cuda.synchronize(dev)
+        c.check(c.lib.rrte_hip_synchronize(c.h))
         a = time.perf_counter()
         for i in range(n):
             go(i)
         torch.cuda.synchronize(dev)
         ts = (time.perf_counter() - a) / n
-        st = c.stats()
-        out[kind] = {"value": round(rays_per_frame / ts / 1e6, 3), "unit": "Mray/s", "ms_per_frame": round(ts * 1e3, 4),
-                     "jit_active": int(st.jit_active)}
         c.check(c.lib.rrte_hip_synchronize(c.h))
+        st = c.stats()
+        rays = rays_per_frame if not frames else prm.width * prm.height * prm.samples_per_pixel + int(st.shadow_rays) / n
+        out[kind] = {"value": round(rays / ts / 1e6, 3), "unit": "Mray/s", "ms_per_frame": round(ts * 1e3, 4),
+                     "jit_active": int(st.jit_active)}
+        if frames:
+            out[kind]["scenes"] = len(frames)
+            out[kind]["upload_host_ms"] = round(st.upload_ms, 4)
         c.close()
+    if "topology_animated" in out:
+        out["topology_animated"]["vs_static_topology"] = round(
+            out["topology_animated"]["ms_per_frame"] / out["topology"]["ms_per_frame"], 4)
     out["note"] = (f"{n} frames each, {F} in flight; jit_active 0 generic / 1 full / 2 topology "
-                   "(include/rrte_hip.h rrte_hip_set_jit)")
+                   "(include/rrte_hip.h rrte_hip_set_jit); topology_animated: a new scene every frame "
+                   "(8-frame value animation, cycled)")
     return out
 
 
@@ -431,7 +447,9 @@ def main():
 
     kinds = None
     if world == 1 and not args.no_stock:
-        kinds = kernel_variants(scene, prm, fulls, sptrs, dev, W * H * prm.samples_per_pixel + shadow // args.steps)
+        anim = [scenes.animate_values(LoweredScene(objs, lights, cam), f) for f in range(8)]
+        kinds = kernel_variants(scene, prm, fulls, sptrs, dev, W * H * prm.samples_per_pixel + shadow // args.steps,
+                                anim=anim)
 
     # the reference's stock config on the generic kernel (rank 0, N=1 only; not the headline)
     stock = None

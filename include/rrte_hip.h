@@ -260,7 +260,7 @@ typedef struct rrte_stats {
     uint64_t shadow_rays;    /* shadow rays actually cast in the last frame    */
     double kernel_ms;        /* ray kernel time of the last frame (HIP events) */
     double gather_ms;        /* RCCL gather + de-interleave time               */
-    double upload_ms;        /* scene H2D time (0 when the scene was cached)   */
+    double upload_ms;        /* host time to lower + enqueue a changed scene (0 when cached; the copy is async) */
     uint64_t frames;         /* frames rendered by this context                */
     uint32_t jit_active;     /* last frame's kernel: 0 generic, 1 full, 2 topology specialisation */
     uint32_t hot_tiles;      /* hot slots the last launch dispatched first: the tiles an earlier launch of

@@ -80,17 +80,16 @@ struct rrte_ctx {
     // ring of kSceneVersions buffer sets, so a scene change uploads into a version no frame in flight
     // reads (Retire) instead of draining the device; d_prims ... mesh_view alias the current version.
     std::vector<unsigned char> scene_key;
+    // One scene version = ONE device allocation holding every array (objects, materials, lights, SDF
+    // nodes, culling spheres, mesh BVH / triangles / normals / permutation at 256-B aligned offsets),
+    // filled by ONE copy from a pinned staging buffer on the upload stream; a launch's stream waits
+    // for that copy's event (once per stream and version), so a scene change never blocks the host
+    // on the device.
     struct SceneBuf {
-        DPrim* d_prims = nullptr; size_t cap_prims = 0;
-        DMaterial* d_mats = nullptr; size_t cap_mats = 0;
-        DLight* d_lights = nullptr; size_t cap_lights = 0;
-        rrte_sdf_node* d_nodes = nullptr; size_t cap_nodes = 0;
-        float4* d_bounds = nullptr; size_t cap_bounds = 0;  // culling spheres, one per object
-        // triangle meshes: BVH nodes, triangle slots, normals, original-order permutation (bvh.hip)
-        float4* d_mesh_nodes = nullptr; size_t cap_mesh_nodes = 0;
-        float4* d_mesh_tris = nullptr; size_t cap_mesh_tris = 0;
-        float4* d_mesh_norms = nullptr; size_t cap_mesh_norms = 0;
-        uint32_t* d_mesh_perm = nullptr; size_t cap_mesh_perm = 0;
+        uint8_t* d_buf = nullptr; size_t cap = 0;
+        uint8_t* h_stage = nullptr; size_t cap_h = 0;  // pinned
+        hipEvent_t ev_up = nullptr;                      // the version's upload copy done
+        std::vector<hipStream_t> ordered;                // streams already made to wait for ev_up
         Retire ret;
     };
     static constexpr int kSceneVersions = 4;
@@ -731,7 +730,8 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         ++c->same_scene_renders;
         return RRTE_OK;
     }
-    (void)st;  // the copies run on the context's upload stream, complete before any launch is enqueued
+    (void)st;  // the copy runs on the context's upload stream; launches wait for its event (issue_launch)
+    const auto t_up0 = std::chrono::steady_clock::now();
 
     for (uint32_t k = 0; k < s->num_mesh_indices; ++k)
         if (s->mesh_indices[k] >= s->num_mesh_vertices)
@@ -762,45 +762,52 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     ++c->scene_gen;
     c->sb_cur = -1;  // (until the upload has completed: a failure below leaves no current version)
     c->scene_key.clear();
-    if ((r = ensure(c, B.d_prims, B.cap_prims, prims.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, B.d_bounds, B.cap_bounds, bounds.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, B.d_mats, B.cap_mats, mats.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, B.d_lights, B.cap_lights, lights.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, B.d_nodes, B.cap_nodes, (size_t)s->num_sdf_nodes)) != RRTE_OK) return r;
-    if ((r = ensure(c, B.d_mesh_nodes, B.cap_mesh_nodes, md.nodes.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, B.d_mesh_tris, B.cap_mesh_tris, md.tris.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, B.d_mesh_norms, B.cap_mesh_norms, md.norms.size())) != RRTE_OK) return r;
-    if ((r = ensure(c, B.d_mesh_perm, B.cap_mesh_perm, md.perm.size())) != RRTE_OK) return r;
+    // one allocation, one staging buffer, one copy (256-B aligned sub-arrays)
+    struct Part { const void* src; size_t bytes; size_t off; };
+    Part parts[9] = {{prims.data(), prims.size() * sizeof(DPrim), 0},
+                     {mats.data(), mats.size() * sizeof(DMaterial), 0},
+                     {lights.data(), lights.size() * sizeof(DLight), 0},
+                     {nodes.data(), bn, 0},
+                     {bounds.data(), bounds.size() * sizeof(float4), 0},
+                     {md.nodes.data(), md.nodes.size() * sizeof(float4), 0},
+                     {md.tris.data(), md.tris.size() * sizeof(float4), 0},
+                     {md.norms.data(), md.norms.size() * sizeof(float4), 0},
+                     {md.perm.data(), md.perm.size() * sizeof(uint32_t), 0}};
+    size_t total = 0;
+    for (Part& pt : parts) {
+        pt.off = total;
+        total += (pt.bytes + 255u) & ~(size_t)255u;
+    }
+    total = std::max<size_t>(total, 256u);
+    // the staging buffer may still feed this version's previous upload if no launch ever read it
+    if (B.ev_up) HIPCHK(c, hipEventSynchronize(B.ev_up));  // (upload stream: copies only, bounded)
+    if ((r = ensure(c, B.d_buf, B.cap, total)) != RRTE_OK) return r;
+    if (B.cap_h < total) {
+        if (B.h_stage) (void)hipHostFree(B.h_stage);  // (its copies have completed: ev_up above)
+        B.h_stage = nullptr;
+        B.cap_h = 0;
+        HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&B.h_stage), total, hipHostMallocDefault));
+        B.cap_h = total;
+    }
+    if (!B.ev_up) HIPCHK(c, hipEventCreateWithFlags(&B.ev_up, hipEventDisableTiming));
+    for (const Part& pt : parts)
+        if (pt.bytes) memcpy(B.h_stage + pt.off, pt.src, pt.bytes);
     if (!c->upload_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking));
     hipStream_t us = c->upload_stream;
-    HIPCHK(c, hipEventRecord(c->ev2, us));
-    auto put = [&](void* dst, const void* src, size_t bytes) -> rrte_status {
-        if (bytes) HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, us));
-        return RRTE_OK;
-    };
-    if ((r = put(B.d_prims, prims.data(), prims.size() * sizeof(DPrim))) != RRTE_OK) return r;
-    if ((r = put(B.d_mats, mats.data(), mats.size() * sizeof(DMaterial))) != RRTE_OK) return r;
-    if ((r = put(B.d_lights, lights.data(), lights.size() * sizeof(DLight))) != RRTE_OK) return r;
-    if ((r = put(B.d_nodes, nodes.data(), bn)) != RRTE_OK) return r;
-    if ((r = put(B.d_bounds, bounds.data(), bounds.size() * sizeof(float4))) != RRTE_OK) return r;
-    if ((r = put(B.d_mesh_nodes, md.nodes.data(), md.nodes.size() * sizeof(float4))) != RRTE_OK) return r;
-    if ((r = put(B.d_mesh_tris, md.tris.data(), md.tris.size() * sizeof(float4))) != RRTE_OK) return r;
-    if ((r = put(B.d_mesh_norms, md.norms.data(), md.norms.size() * sizeof(float4))) != RRTE_OK) return r;
-    if ((r = put(B.d_mesh_perm, md.perm.data(), md.perm.size() * sizeof(uint32_t))) != RRTE_OK) return r;
-    HIPCHK(c, hipEventRecord(c->ev0, us));
-    // the staging vectors die at return, and launches enqueued after this call must see the bytes: the
-    // upload stream holds nothing but these copies, so this wait is bounded by the transfer
-    HIPCHK(c, hipStreamSynchronize(us));
-    float ms = 0.0f;
-    (void)hipEventElapsedTime(&ms, c->ev2, c->ev0);
-    *upload_ms = ms;
+    HIPCHK(c, hipMemcpyAsync(B.d_buf, B.h_stage, total, hipMemcpyHostToDevice, us));
+    HIPCHK(c, hipEventRecord(B.ev_up, us));
+    B.ordered.clear();
+    // host time to lower the scene and enqueue its upload (the copy itself is asynchronous)
+    *upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_up0).count();
+    uint8_t* d = B.d_buf;
+    c->d_prims = reinterpret_cast<DPrim*>(d + parts[0].off);
+    c->d_mats = reinterpret_cast<DMaterial*>(d + parts[1].off);
+    c->d_lights = reinterpret_cast<DLight*>(d + parts[2].off);
+    c->d_nodes = reinterpret_cast<rrte_sdf_node*>(d + parts[3].off);
+    c->d_bounds = reinterpret_cast<float4*>(d + parts[4].off);
+    c->mesh_view = MeshView{reinterpret_cast<float4*>(d + parts[5].off), reinterpret_cast<float4*>(d + parts[6].off),
+                            reinterpret_cast<float4*>(d + parts[7].off), reinterpret_cast<uint32_t*>(d + parts[8].off)};
     c->sb_cur = nx;
-    c->d_prims = B.d_prims;
-    c->d_mats = B.d_mats;
-    c->d_lights = B.d_lights;
-    c->d_nodes = B.d_nodes;
-    c->d_bounds = B.d_bounds;
-    c->mesh_view = MeshView{B.d_mesh_nodes, B.d_mesh_tris, B.d_mesh_norms, B.d_mesh_perm};
     c->h_prims = prims;
     c->h_bounds = bounds;
     c->h_mats = mats;
@@ -1348,7 +1355,14 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     // 64-thread workgroups: (tile column, frame, tile row or slot row), KParams::hot
     const bool profile = plan_tile_order(c, L, jk ? (const void*)jk->fn : nullptr, st);
     c->stats.hot_tiles = L.k.hot_n;
-    if (c->sb_cur >= 0) c->sb[c->sb_cur].ret.use(st);  // the launch reads the current scene version
+    if (c->sb_cur >= 0) {  // the launch reads the current scene version: after its upload, tracked until retired
+        rrte_ctx::SceneBuf& B = c->sb[c->sb_cur];
+        if (std::find(B.ordered.begin(), B.ordered.end(), st) == B.ordered.end()) {
+            HIPCHK(c, hipStreamWaitEvent(st, B.ev_up, 0));
+            B.ordered.push_back(st);
+        }
+        B.ret.use(st);
+    }
     c->launched.use(st);
     const dim3 grid(L.gx, L.k.nframes, L.gy), block(kBlockThreads);
     if (jk) {
@@ -1603,10 +1617,9 @@ void rrte_hip_destroy(rrte_ctx* c) {
     c->jit_pending.clear();  // joins background compiles
     for (auto& kv : c->jit_cache) jit_release(kv.second);
     for (auto& B : c->sb) {
-        void* sbufs[] = {B.d_prims, B.d_mats, B.d_lights, B.d_nodes, B.d_bounds, B.d_mesh_nodes, B.d_mesh_tris,
-                         B.d_mesh_norms, B.d_mesh_perm};
-        for (void* b : sbufs)
-            if (b) (void)hipFree(b);
+        if (B.d_buf) (void)hipFree(B.d_buf);
+        if (B.h_stage) (void)hipHostFree(B.h_stage);
+        if (B.ev_up) (void)hipEventDestroy(B.ev_up);
         destroy_events(B.ret);
     }
     void* bufs[] = {c->d_rgba, c->d_f32, c->d_counters, c->d_gather, c->d_full};

@@ -236,3 +236,27 @@ SCENES = {
     "deformation-stress": deformation_stress,
     "mesh-demo": mesh_demo,
 }
+
+
+def animate_values(sc, f):
+    """Frame f of a value-only animation of a lowered scene (rrte_amd.LoweredScene), in place: every
+    SDF leaf moves in x and z, every smooth op's k grows, every light moves down and dims, every
+    material's red channel rises -- the topology (object kinds, SDF structure, light kinds) stays, so
+    one topology-specialised kernel serves every frame (the reference re-renders after
+    scene_mut().update(dt) every frame, examples/sdf-showcase/src/main.rs:133-139)."""
+    import numpy as np
+    for i in range(sc.ir.num_sdf_nodes):
+        n = sc.nodes[i]
+        if n.op < 32:  # leaves: centre x, z
+            n.f[0] = np.float32(n.f[0] + 0.15 * f)
+            n.f[2] = np.float32(n.f[2] - 0.1 * f)
+        elif 35 <= n.op <= 37:  # smooth ops: k
+            n.f[0] = np.float32(n.f[0] * (1.0 + 0.2 * f))
+    for i in range(sc.ir.num_lights):
+        L = sc.lights[i]
+        L.position[1] = np.float32(L.position[1] - 0.7 * f)
+        L.intensity = np.float32(L.intensity * (1.0 - 0.05 * f))
+    for i in range(sc.ir.num_materials):
+        m = sc.mats[i]
+        m.albedo[0] = np.float32(min(1.0, m.albedo[0] + 0.05 * f))
+    return sc

@@ -24,22 +24,9 @@ def test_topology_kernels_match_oracle(name, mode, monkeypatch):
 
 
 def _animate(sc: LoweredScene, f: int):
-    """Frame f of a value-only animation: every SDF leaf and smooth op moves/changes, every light moves
-    and dims, every material changes colour -- the topology stays."""
-    for i in range(sc.ir.num_sdf_nodes):
-        n = sc.nodes[i]
-        if n.op < 32:  # leaves: centre x, z
-            n.f[0] = np.float32(n.f[0] + 0.15 * f)
-            n.f[2] = np.float32(n.f[2] - 0.1 * f)
-        elif 35 <= n.op <= 37:  # smooth ops: k
-            n.f[0] = np.float32(n.f[0] * (1.0 + 0.2 * f))
-    for i in range(sc.ir.num_lights):
-        L = sc.lights[i]
-        L.position[1] = np.float32(L.position[1] - 0.7 * f)
-        L.intensity = np.float32(L.intensity * (1.0 - 0.05 * f))
-    for i in range(sc.ir.num_materials):
-        m = sc.mats[i]
-        m.albedo[0] = np.float32(min(1.0, m.albedo[0] + 0.05 * f))
+    """Frame f of a value-only animation (rrte_amd.scenes.animate_values): every SDF leaf and smooth op
+    moves/changes, every light moves and dims, every material changes colour -- the topology stays."""
+    scenes.animate_values(sc, f)
 
 
 def _render(ctx, sc, prm, w, h):
@@ -99,3 +86,40 @@ def test_topology_change_leaves_the_topology_kernel(monkeypatch):
     assert st.jit_active == 1
     assert np.array_equal(lin.view(np.uint32), want.view(np.uint32)) and int(st.shadow_rays) == wsh
     ctx.close()
+
+
+@pytest.mark.parametrize("jit_topo", ["1", "2"])
+def test_animation_in_flight_is_exact(jit_topo, monkeypatch):
+    """a scene change per frame with frames in flight -- 5 animation frames issued on 4
+    streams without a synchronisation between them (each scene uploaded into the next version of the
+    scene ring while the earlier frames still read theirs) -- every frame's linear image bit-exact
+    against the oracle and the shadow-ray total exact; topology kernel forced (1) or adaptive (2)."""
+    import torch
+    monkeypatch.setenv("RRTE_JIT_TOPO", jit_topo)
+    w, h = 160, 96
+    objs, lights, cam, cfg = scenes.sdf_showcase(w, h)
+    prm = cfg.lower()
+    prm.flags |= abi.FLAG_F32_LINEAR
+    frames = [_animate_copy(objs, lights, cam, f) for f in range(5)]
+    want = [oracle.render(sc, prm, nthreads=16, linear=True) for sc in frames]
+    ctx = Context(0, jit=abi.JIT_ON)
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    outs = [torch.zeros(w * h * 4, dtype=torch.float32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()
+    for rnd in range(2):  # round 0 compiles; round 1 runs the animation on warm kernels
+        for i, sc in enumerate(frames):
+            ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), None, outs[i].data_ptr(),
+                                                    C.c_void_p(streams[i % 4].cuda_stream)))
+        ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+        assert int(ctx.stats().shadow_rays) == sum(wsh for _, _, wsh in want)
+        for i, o in enumerate(outs):
+            got = o.cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, want[i][1].view(np.uint32)), f"round {rnd} frame {i}"
+    assert ctx.stats().jit_active == 2
+    ctx.close()
+
+
+def _animate_copy(objs, lights, cam, f):
+    sc = LoweredScene(objs, lights, cam)
+    _animate(sc, f)
+    return sc
