@@ -71,6 +71,9 @@ struct FrameCam {
     // 4 = 16x16, four 8x8 workgroups); a tile outside it cannot hit object i with a camera ray.  0: off.
     uint32_t tile_cull, tile_n;
     uint32_t tile_rect[32];
+    // KParams::out_image_rows launches: this frame's RGBA8 frame buffer (the batched multi-GPU root
+    // renders its own bands straight into each frame's caller buffer)
+    uint32_t* out;
 };
 
 // A launch renders up to kMaxLaunchFrames frames of one scene with the same parameters and their own
@@ -108,8 +111,9 @@ struct KParams {
     uint32_t* tile_cost;     // non-null: frame 0's workgroups store their duration (100 MHz ticks) at [y * tiles_x + x]
     const uint32_t* hot;     // device tile list (hot_n words; immutable while launches use it)
     uint32_t tiles_x, hot_n;
-    // Output rows: 0 = this launch's rows packed (row r at r * width), 1 = at their image rows
-    // (image_row(r) * width: a multi-GPU root renders its own bands straight into the final frame)
+    // Output rows: 0 = this launch's rows packed (row r at r * width, frame z at out + z * frame_stride),
+    // 1 = at their image rows of frame z's own buffer cam[z].out (image_row(r) * width: a multi-GPU
+    // root renders its own bands straight into the final frames; RGBA8 only)
     uint32_t out_image_rows;
     FrameCam cam[kMaxLaunchFrames];
 };

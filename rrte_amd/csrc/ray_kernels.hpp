@@ -1970,7 +1970,9 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     if (!tile.run) return;
     // frame tile.z of the launch: its camera, its output (multi-frame launches have no f32 output)
     const FrameCam& cm = kp.cam[tile.z];
-    if (out_rgba8 && tile.z)
+    if (kp.out_image_rows)
+        out_rgba8 = cm.out;
+    else if (out_rgba8 && tile.z)
         out_rgba8 = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out_rgba8) + tile.z * kp.frame_stride);
     // RRTE_DEBUG bit 4 (diagnostics, tools/wave_times.py): per-wave start / duration from the 100 MHz
     // wall clock into the f32 buffer instead of colours
@@ -2123,7 +2125,8 @@ __global__ __launch_bounds__(kBlockThreads) void ray_kernel(KParams kp, SceneVie
 }
 
 // Root-side de-interleave after the RCCL gather: the gathered buffer holds, per rank (rank_stride
-// bytes each), that rank's packed rows of `gridDim.z` frames back to back (frame_stride bytes each,
+// bytes each; rank `skip_rank`'s rows -- the root's, rendered in place -- are skipped, ~0u for none),
+// that rank's packed rows of `gridDim.z` frames back to back (frame_stride bytes each,
 // `rows_cap` rows of RGBA8 or RGB24 per frame); frame z goes to full[z] (one frame per launch for
 // per-frame gathers, a batch's frames for rrte_hip_set_gather_batch).  RGB24 slabs are expanded
 // with alpha 255 (the host proved every alpha byte is 255).  VEC4: each lane moves 4 pixels (three
@@ -2137,10 +2140,12 @@ template <bool RGB24, bool VEC4>
 __global__ __launch_bounds__(256) void deinterleave_batch_kernel(const uint8_t* __restrict__ gathered,
                                                                  DeinterleaveTargets t, uint32_t width,
                                                                  uint32_t band_rows, uint32_t nranks,
-                                                                 size_t rank_stride, size_t frame_stride) {
+                                                                 size_t rank_stride, size_t frame_stride,
+                                                                 uint32_t skip_rank) {
     const uint32_t y = blockIdx.y;
     const uint32_t band = y / band_rows, w = y - band * band_rows;
     const uint32_t rank = band % nranks, local_band = band / nranks;
+    if (rank == skip_rank) return;  // the root's own bands: rendered into the frame in place
     const uint32_t lr = local_band * band_rows + w;
     constexpr uint32_t bpp = RGB24 ? 3u : 4u;
     const uint8_t* src = gathered + (size_t)rank * rank_stride + (size_t)blockIdx.z * frame_stride +

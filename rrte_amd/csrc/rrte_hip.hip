@@ -117,6 +117,7 @@ struct rrte_ctx {
     // multi-GPU
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    int comm_size = 0;               // ranks of the RCCL communicator (nranks may be emulated, RRTE_EMULATE_RANK)
     uint32_t* d_gather = nullptr; size_t cap_gather = 0;
     uint32_t* d_full = nullptr; size_t cap_full = 0;
     static constexpr int kSlabs = 16;  // per-frame gathers (batch 1) that may be in flight at once
@@ -141,7 +142,7 @@ struct rrte_ctx {
     struct Batch {
         uint32_t n = 0, cap = 0;             // frames planned into it / frames it was opened for
         uint32_t rendered = 0;               // frames [0, rendered) already launched into the send slab
-        bool inplace = false;                // root, rendered at the flush: into its slot of the receive slab
+        bool in_place = false;               // root: its bands rendered straight into the frames (RGBA8)
         uint32_t width = 0, height = 0, band = 0;
         int root = 0;
         bool rgb24 = false;
@@ -193,7 +194,9 @@ struct rrte_ctx {
     bool env_tile_cull = true;    // RRTE_TILE_CULL=0: no camera-ray tile culling (A/B, tests)
     bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
     bool env_gather_rgba = false;   // RRTE_GATHER_RGB24=0: gather slabs always RGBA8
-    bool env_gather_inplace = true; // RRTE_GATHER_INPLACE=0: the root's batch share through the send slab
+    bool env_gather_self = false;   // RRTE_GATHER_SELF=1 (tests): the root sends its own bands to itself
+                                    // through RCCL and expands them like a peer's (the 1-GPU check of the
+                                    // send / recv / expand path)
     uint32_t env_guard_leaves = 2;  // RRTE_CSG_GUARDS: 0 = off, N = smallest guarded operand (leaves)
     bool env_wg256 = false;           // RRTE_WG64=0: specialised kernels in 256-thread workgroups (A/B only)
     int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
@@ -1556,7 +1559,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_FAULT_STALL_GATHER")) c->fault_stall_at = strtoull(g, nullptr, 0);
     if (const char* g = getenv("RRTE_BATCH_SLABS"); g && *g)
         c->batch_slabs = std::max(1, std::min(rrte_ctx::kBatchSlabs, (int)strtol(g, nullptr, 0)));
-    if (const char* g = getenv("RRTE_GATHER_INPLACE")) c->env_gather_inplace = g[0] != '0';
+    if (const char* g = getenv("RRTE_GATHER_SELF")) c->env_gather_self = g[0] == '1';
     if (const char* g = getenv("RRTE_COMM_PRIORITY")) c->env_comm_priority = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
@@ -1917,6 +1920,7 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
     }
     c->nranks = nranks;
     c->rank = rank;
+    c->comm_size = nranks;
     if (nranks == 1 && c->emu_nranks > 1) {
         // RRTE_EMULATE_RANK=N:R with a 1-rank communicator (diagnostic, one GPU): the gather path lays
         // frames out as rank R of N -- R's bands rendered into its slab slice, the 1-rank gather moving
@@ -1952,20 +1956,20 @@ bool slab_rgb24(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_par
 // De-interleave `n` gathered frames (ray_kernels.hpp deinterleave_batch_kernel) on `st`.
 static rrte_status deinterleave(rrte_ctx* c, hipStream_t st, const uint8_t* gathered, const DeinterleaveTargets& t,
                                 uint32_t n, uint32_t width, uint32_t height, uint32_t band, bool rgb24,
-                                size_t rank_stride, size_t frame_stride) {
+                                size_t rank_stride, size_t frame_stride, uint32_t skip_rank = ~0u) {
     bool vec4 = width % 4u == 0;
     for (uint32_t j = 0; j < n; ++j) vec4 = vec4 && reinterpret_cast<uintptr_t>(t.full[j]) % 16u == 0;
     const uint32_t per = vec4 ? 1024u : 256u;  // pixels one workgroup moves per pass
     const dim3 dg(std::min((width + per - 1) / per, 8u), height, n), db(256);
     const uint32_t nr = (uint32_t)c->nranks;
     if (rgb24 && vec4)
-        hipLaunchKernelGGL((deinterleave_batch_kernel<true, true>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride);
+        hipLaunchKernelGGL((deinterleave_batch_kernel<true, true>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride, skip_rank);
     else if (rgb24)
-        hipLaunchKernelGGL((deinterleave_batch_kernel<true, false>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride);
+        hipLaunchKernelGGL((deinterleave_batch_kernel<true, false>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride, skip_rank);
     else if (vec4)
-        hipLaunchKernelGGL((deinterleave_batch_kernel<false, true>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride);
+        hipLaunchKernelGGL((deinterleave_batch_kernel<false, true>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride, skip_rank);
     else
-        hipLaunchKernelGGL((deinterleave_batch_kernel<false, false>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride);
+        hipLaunchKernelGGL((deinterleave_batch_kernel<false, false>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride, skip_rank);
     HIPCHK(c, hipGetLastError());
     return RRTE_OK;
 }
@@ -1979,11 +1983,11 @@ static rrte_status render_batch(rrte_ctx* c, bool at_flush) {
     if (b.rendered >= b.n) return RRTE_OK;
     HostSection hs(c);
     const int k = c->bslot;
-    // The root renders a batch that is first rendered at its flush (its frame count final) straight
-    // into its own slot of the receive slab, and the gather runs in place: no self-copy of the root's
-    // share (RRTE_GATHER_INPLACE=0: always through the send slab, A/B)
-    if (b.rendered == 0) b.inplace = at_flush && c->rank == b.root && c->env_gather_inplace;
-    uint8_t* base = b.inplace ? c->d_brecv[k] + (size_t)b.root * ((size_t)b.n * b.slice) : c->d_bsend[k];
+    (void)at_flush;
+    // The root renders its own bands straight into each frame's caller buffer at their image rows
+    // (RGBA8; FrameCam::out): nothing of the root's share is copied, gathered or expanded.  Peers
+    // render into the send slab (packed rows, RGB24 when alpha is provably 255).
+    uint8_t* base = b.in_place ? nullptr : c->d_bsend[k];
     hipStream_t rs = c->render_stream[k];
     // the renders follow the frames' caller streams (scene uploads, the callers' own prior work) and
     // the slab's previous batch (its gather reads the send slab)
@@ -2000,7 +2004,9 @@ static rrte_status render_batch(rrte_ctx* c, bool at_flush) {
         memcpy(L.k.cam, b.cam + j0, nf * sizeof(FrameCam));
         L.k.nframes = nf;
         L.k.frame_stride = b.slice;
-        uint8_t* dst = base + (size_t)j0 * b.slice;
+        L.k.out_image_rows = b.in_place ? 1u : 0u;
+        if (b.in_place) L.k.flags &= ~kFlagSlabRgb24;
+        uint8_t* dst = b.in_place ? nullptr : base + (size_t)j0 * b.slice;
         rrte_status r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, rs);
         if (r != RRTE_OK) return r;
     }
@@ -2159,15 +2165,27 @@ static rrte_status flush_batch(rrte_ctx* c) {
             HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->last_gather_ev, 0));
         hs.lap(4);
         if ((r = before_collective(c, c->comm_stream)) != RRTE_OK) return r;
-        if (!(c->env_diag_skip & 1u))
-            NCCLCHK(c, ncclGather(b.inplace ? c->d_brecv[k] + (size_t)b.root * count : c->d_bsend[k], c->d_brecv[k],
-                                  count, ncclUint8, b.root, c->comm, c->comm_stream));
+        // every peer's slab to the root: grouped point-to-point (the root's own bands never move); with
+        // a 1-rank communicator (emulated ranks, RRTE_EMULATE_RANK) there is no peer, RRTE_GATHER_SELF
+        // routes the root's bands through RCCL to itself
+        const bool self_only = c->comm_size == 1;  // (no real peer: only the root's RRTE_GATHER_SELF round trip)
+        if (!(c->env_diag_skip & 1u) && (!self_only || (!b.in_place && c->rank == b.root))) {
+            NCCLCHK(c, ncclGroupStart());
+            if (c->rank == b.root) {
+                for (int q = 0; q < c->comm_size; ++q)
+                    if (q != b.root || !b.in_place)
+                        NCCLCHK(c, ncclRecv(c->d_brecv[k] + (size_t)q * count, count, ncclUint8, q, c->comm, c->comm_stream));
+            }
+            if (c->rank != b.root || !b.in_place)
+                NCCLCHK(c, ncclSend(c->d_bsend[k], count, ncclUint8, b.root, c->comm, c->comm_stream));
+            NCCLCHK(c, ncclGroupEnd());
+        }
         hs.lap(5);
-        if (c->rank == b.root && !(c->env_diag_skip & 2u)) {
+        if (c->rank == b.root && !(c->env_diag_skip & 2u) && (c->nranks > 1 || !b.in_place)) {
             DeinterleaveTargets t{};
             for (uint32_t j = 0; j < b.n; ++j) t.full[j] = b.full[j];
             if ((r = deinterleave(c, c->comm_stream, c->d_brecv[k], t, b.n, b.width, b.height, b.band, b.rgb24, count,
-                                  b.slice)) != RRTE_OK)
+                                  b.slice, b.in_place ? (uint32_t)b.root : ~0u)) != RRTE_OK)
                 return r;
         }
         hs.lap(6);
@@ -2252,6 +2270,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             b.rgb24 = rgb24;
             b.slice = slice;
             b.plan = L;
+            b.in_place = c->rank == root && !c->env_gather_self;
             // every rank holds a receive slab too (the root's is the only one written)
             const size_t send = (size_t)b.cap * slice, recv = send * (size_t)c->nranks;
             if (c->cap_bsend[k] < send || c->cap_brecv[k] < recv) {
@@ -2266,6 +2285,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         }
         hs.lap(2);
         b.cam[b.n] = L.k.cam[0];
+        b.cam[b.n].out = static_cast<uint32_t*>(d_full);
         b.full[b.n] = static_cast<uint32_t*>(d_full);
         uint32_t i = 0;
         while (i < b.nsrc && b.src[i] != st) ++i;

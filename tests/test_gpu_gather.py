@@ -1,6 +1,7 @@
 """Multi-GPU frame path on one GPU: a 1-rank RCCL communicator with RRTE_FORCE_GATHER=1 drives
-rrte_hip_render_gather(_async) through the real band render -> ncclGather -> de-interleave
-sequence, with frames in flight on three streams, gathered per frame or in batches of 3 or 8
+rrte_hip_render_gather(_async) through the real band render -> RCCL (ncclGather per frame; grouped
+send / receive per batch, the root's own bands rendered in place or, RRTE_GATHER_SELF, sent to
+itself) -> expansion sequence, with frames in flight on three streams, gathered per frame or in batches of 3 or 8
 (rrte_hip_set_gather_batch: one ncclGather for a batch of frames on the comm stream; 7 frames leave
 a partial batch for the flush), and with the (now ignored) RRTE_FLAG_GATHER_OVERLAP.  Every frame
 must equal the plain single-context render bit for bit.  (N > 1 needs more GPUs than the
@@ -38,18 +39,25 @@ def _frames(n, w=320, h=200, alpha=None, first=0):
     return out
 
 
+@pytest.mark.parametrize("route", ["in_place", "self"])
 @pytest.mark.parametrize("batch", [1, 3, 8])
 @pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
-def test_gather_path_matches_plain_render(overlap, jit, batch, monkeypatch):
+def test_gather_path_matches_plain_render(overlap, jit, batch, route, monkeypatch):
+    """route in_place: the batched root renders its bands straight into the frames; self
+    (RRTE_GATHER_SELF=1): the root's bands go through the peers' path -- packed slab, RCCL send and
+    receive (to itself), expansion into the frames -- the path every peer's bands take at N > 1."""
+    if route == "self":
+        monkeypatch.setenv("RRTE_GATHER_SELF", "1")
     _check_gather(overlap, jit, batch, monkeypatch, None)
 
 
 @pytest.mark.parametrize("alpha,rgb24", [(None, "0"), ("material", "1"), ("spp2", "1")])
 def test_gather_slab_formats(alpha, rgb24, monkeypatch):
     """RGBA8 slabs when forced (RRTE_GATHER_RGB24=0) or when some alpha byte is not 255; every
-    frame still equal to the plain render, alpha bytes included."""
+    frame still equal to the plain render, alpha bytes included (the slab path: RRTE_GATHER_SELF)."""
     monkeypatch.setenv("RRTE_GATHER_RGB24", rgb24)
+    monkeypatch.setenv("RRTE_GATHER_SELF", "1")
     _check_gather(True, abi.JIT_ON, 1, monkeypatch, alpha)
     _check_gather(False, abi.JIT_ON, 4, monkeypatch, alpha)
 

@@ -7,6 +7,7 @@ R=$GRAFT_REPO_ROOT
 STEPS=${1:-20}; N=${2:-8}
 OUT=$R/gpurun_out/emutrace_${N}_$STEPS
 rm -rf $OUT; mkdir -p $OUT
+export GPU_MAX_HW_QUEUES=32  # (under rocprofv3 HIP starts before bench.py could set it)
 cd /tmp && export TMPDIR=/tmp
 RRTE_HOST_PROFILE=1 RRTE_BENCH_GATHER=1 RRTE_EMULATE_RANK=$N:0 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- python3 $R/bench.py --no-cpu --no-stock --steps $STEPS > $OUT/run.log 2>&1 || { tail $OUT/run.log; exit 1; }
 tail -1 $OUT/run.log | cut -c1-200
