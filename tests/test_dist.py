@@ -1,8 +1,11 @@
-"""Multi-rank row-band composition on CPU (gloo, world_size 2 and 3): each rank renders its
-interleaved bands (the oracle stands in for the per-rank kernel), packs them exactly as
-ray_kernel does for a rank, the frame is gathered to rank 0 and de-interleaved with the
-mapping of deinterleave_kernel; the result must equal the single-process frame bit-for-bit.
-The GPU path runs the same mapping with ncclGather (RCCL/xGMI) inside librrte_hip."""
+"""Multi-rank row-band composition on CPU (gloo, world_size 2 and 3), in the layout of the batched GPU
+path (rrte_hip.hip render_batch / flush_batch): each rank renders its interleaved bands (the oracle
+stands in for the per-rank kernel); the ROOT writes its own bands straight into the frame at their
+image rows (KParams::out_image_rows), every PEER packs its rows as ray_kernel does for a rank -- RGB24,
+the alpha byte dropped, since LAMBERT_SHADOW proves it 255 -- and sends the slab to the root point to
+point (ncclSend / ncclRecv there, dist.send / recv here), and the root expands only the peers' rows
+with the mapping of deinterleave_batch_kernel (alpha 255 restored).  The result must equal the
+single-process frame bit for bit."""
 import os
 import socket
 
@@ -51,18 +54,28 @@ def _worker(rank, n, port, scene_name, q):
             full, _, sh = oracle.render(sc, cfg.lower(), nthreads=1, rows=(y, y + 1), want_f32=False)
             packed[i] = full.reshape(H, W, 4)[y]
             shadow += sh
-        t = torch.from_numpy(packed.reshape(-1))
-        gathered = [torch.zeros_like(t) for _ in range(n)] if rank == 0 else None
-        dist.gather(t, gathered, dst=0)
         tot = torch.tensor([shadow], dtype=torch.int64)
         dist.all_reduce(tot)
-        if rank == 0:
-            g = torch.stack(gathered).numpy().reshape(n, cap, W, 4)
+        if rank != 0:
+            rgb24 = np.ascontiguousarray(packed[..., :3])  # the slab format (kFlagSlabRgb24)
+            assert (packed[:len(img_rows), :, 3] == 255).all()  # alpha provably 255 (slab_rgb24)
+            dist.send(torch.from_numpy(rgb24.reshape(-1)), dst=0)
+        else:
             out = np.zeros((H, W, 4), np.uint8)
-            for y in range(H):  # deinterleave_kernel
+            for i, y in enumerate(img_rows):  # the root's own bands, in place
+                out[y] = packed[i]
+            slabs = {}
+            for r in range(1, n):
+                t = torch.zeros(cap * W * 3, dtype=torch.uint8)
+                dist.recv(t, src=r)
+                slabs[r] = t.numpy().reshape(cap, W, 3)
+            for y in range(H):  # deinterleave_batch_kernel<RGB24>: peers' rows only (skip_rank = root)
                 band, w = divmod(y, BAND)
                 r, lb = band % n, band // n
-                out[y] = g[r, lb * BAND + w]
+                if r == 0:
+                    continue
+                out[y, :, :3] = slabs[r][lb * BAND + w]
+                out[y, :, 3] = 255
             ref, _, ref_sh = oracle.render(sc, cfg.lower(), nthreads=2, want_f32=False)
             q.put((np.array_equal(out, ref.reshape(H, W, 4)), int(tot.item()), ref_sh))
     finally:
