@@ -58,6 +58,9 @@ def test_local_calls_render_but_do_not_close_a_batch(monkeypatch):
     gathered -- their outputs stay untouched -- until the batch fills; then every frame is exact."""
     import torch
     monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    # the root's bands through the slab + RCCL path (a single-rank root otherwise renders its bands
+    # straight into the frames at render time, so the outputs would not show whether a collective ran)
+    monkeypatch.setenv("RRTE_GATHER_SELF", "1")
     frames = _frames(4)
     objs, lights, cam, cfg = scenes.basic_demo(W, H, mode="lambert_shadow")
     preview = (LoweredScene(objs, lights, cam), cfg.lower())
