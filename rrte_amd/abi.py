@@ -134,6 +134,9 @@ EXPORTS = {
     "rrte_hip_render_gather": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_int, _P]),
     "rrte_hip_render_gather_async": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_int, _P, _P]),
     "rrte_hip_band_rows_for_rank": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_int, C.c_int]),
+    "rrte_hip_band_layout": (C.c_int, [C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_int, C.c_int,
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "rrte_hip_band_rows_for_rank_ex": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_uint32, C.c_uint32]),
     "rrte_hip_set_gather_batch": (C.c_int, [_P, C.c_uint32]),
     "rrte_hip_flush": (C.c_int, [_P]),
     "rrte_hip_set_comm_timeout": (C.c_int, [_P, C.c_uint32]),

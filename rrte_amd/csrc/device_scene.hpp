@@ -86,6 +86,32 @@ __host__ __device__ constexpr uint32_t hot_pack(uint32_t x, uint32_t y) { return
 __host__ __device__ constexpr uint32_t hot_x(uint32_t h) { return h & 0xffffu; }
 __host__ __device__ constexpr uint32_t hot_y(uint32_t h) { return h >> 16; }
 
+// Multi-GPU row-band partition (DESIGN.md §5 "Band partition").  The image is cut into
+// bands of `band_rows` rows.  The first `sky` bands -- rows no object can reach, judged on the host
+// from the camera-ray tile rectangles, so every camera ray there misses (the cheapest rows of the
+// frame) -- belong to rank 0 (the root: its rows never cross a link); the remaining bands go round
+// robin over the ranks, the root included only when `root_share` is 1.  sky = 0, root_share = 1 is
+// the plain interleave band % nranks == rank.  Which rank renders a band never changes a pixel.
+struct BandMap {
+    uint32_t band_rows, nranks, sky, root_share;
+};
+// The image band of `rank`'s local band lb.
+__host__ __device__ constexpr uint32_t band_of_local(const BandMap& m, uint32_t rank, uint32_t lb) {
+    const uint32_t L = m.nranks - 1u + m.root_share;  // bands per round-robin cycle
+    return rank == 0u ? (lb < m.sky ? lb : m.sky + (lb - m.sky) * L) : m.sky + (rank - 1u + m.root_share) + lb * L;
+}
+// The rank owning image band b and its local band index there.
+__host__ __device__ constexpr uint32_t band_owner(const BandMap& m, uint32_t b, uint32_t& lb) {
+    if (b < m.sky || m.nranks <= 1u) {
+        lb = b;
+        return 0u;
+    }
+    const uint32_t L = m.nranks - 1u + m.root_share, q = b - m.sky, slot = q % L;
+    const uint32_t owner = m.root_share ? slot : slot + 1u;
+    lb = owner == 0u ? m.sky + q / L : q / L;
+    return owner;
+}
+
 // Per-launch constants, passed by value (kernel arguments land in SGPRs).
 struct KParams {
     uint32_t width, height;
@@ -96,6 +122,7 @@ struct KParams {
     uint32_t rows;           // rows this launch renders
     uint32_t band_rows;      // 0 = identity mapping (+ row0)
     uint32_t nranks, rank;
+    uint32_t sky_bands, root_share;  // band partition (BandMap) of multi-GPU frames
     uint32_t row0;           // first image row of this launch (row-chunked blocking renders; band_rows == 0)
     float bg[4];
     float t_min, bias, inv_gamma, inv_spp;

@@ -1907,8 +1907,9 @@ __device__ __forceinline__ uint32_t gamma22_u8(float c) {
 // Map this launch's local row to the image row (band interleave, §8e).
 __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
     if (kp.band_rows == 0) return r + kp.row0;
-    uint32_t b = r / kp.band_rows, w = r - b * kp.band_rows;
-    return (b * kp.nranks + kp.rank) * kp.band_rows + w;
+    const uint32_t b = r / kp.band_rows, w = r - b * kp.band_rows;
+    const BandMap m{kp.band_rows, kp.nranks, kp.sky_bands, kp.root_share};
+    return band_of_local(m, kp.rank, b) * kp.band_rows + w;
 }
 
 // Camera-ray tile culling mask of this wave's 8x8 tile (kp.tile_cull = 3) or the 16x16
@@ -2139,12 +2140,13 @@ struct DeinterleaveTargets {
 template <bool RGB24, bool VEC4>
 __global__ __launch_bounds__(256) void deinterleave_batch_kernel(const uint8_t* __restrict__ gathered,
                                                                  DeinterleaveTargets t, uint32_t width,
-                                                                 uint32_t band_rows, uint32_t nranks,
-                                                                 size_t rank_stride, size_t frame_stride,
+                                                                 BandMap bm, size_t rank_stride, size_t frame_stride,
                                                                  uint32_t skip_rank) {
     const uint32_t y = blockIdx.y;
+    const uint32_t band_rows = bm.band_rows;
     const uint32_t band = y / band_rows, w = y - band * band_rows;
-    const uint32_t rank = band % nranks, local_band = band / nranks;
+    uint32_t local_band = 0;
+    const uint32_t rank = band_owner(bm, band, local_band);
     if (rank == skip_rank) return;  // the root's own bands: rendered into the frame in place
     const uint32_t lr = local_band * band_rows + w;
     constexpr uint32_t bpp = RGB24 ? 3u : 4u;

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <future>
+#include <limits>
 #include <thread>
 #include <atomic>
 #include <condition_variable>
@@ -144,6 +145,7 @@ struct rrte_ctx {
         uint32_t rendered = 0;               // frames [0, rendered) already launched into the send slab
         bool in_place = false;               // root: its bands rendered straight into the frames (RGBA8)
         uint32_t width = 0, height = 0, band = 0;
+        BandMap bm{};                        // the batch's band partition (a frame with another closes it)
         int root = 0;
         bool rgb24 = false;
         size_t slice = 0;                    // bytes of one frame of one rank (256-B aligned)
@@ -194,6 +196,7 @@ struct rrte_ctx {
     bool env_tile_cull = true;    // RRTE_TILE_CULL=0: no camera-ray tile culling (A/B, tests)
     bool env_force_gather = false;  // RRTE_FORCE_GATHER=1
     bool env_gather_rgba = false;   // RRTE_GATHER_RGB24=0: gather slabs always RGBA8
+    bool env_band_sky = true;       // RRTE_BAND_SKY=0: the plain band interleave (band_layout)
     bool env_gather_self = false;   // RRTE_GATHER_SELF=1 (tests): the root sends its own bands to itself
                                     // through RCCL and expands them like a peer's (the 1-GPU check of the
                                     // send / recv / expand path)
@@ -278,6 +281,15 @@ struct rrte_ctx {
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
     // per launch, so the version pool wraps within a few frames)
     bool env_test_recycle = false;
+    // band partition of the last multi-GPU frame (frame_band_map)
+    struct {
+        bool valid = false;
+        uint64_t gen = 0;
+        uint32_t w = 0, h = 0, band = 0;
+        int nranks = 0, root = 0;
+        rrte_camera cam{};
+        BandMap m{};
+    } band_cache;
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
     struct {
         bool valid = false;
@@ -849,6 +861,8 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     k.band_rows = c->nranks > 1 ? p->band_rows : 0;
     k.nranks = (uint32_t)c->nranks;
     k.rank = (uint32_t)c->rank;
+    k.sky_bands = 0;  // (the plain interleave; plan_launch applies a frame's BandMap)
+    k.root_share = 1;
     memcpy(k.bg, p->background, sizeof k.bg);
     k.t_min = p->t_min;
     k.bias = p->shadow_bias;
@@ -910,7 +924,13 @@ void fill_tile_rects(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_para
     memcpy(tc.rect, kk.cam[0].tile_rect, sizeof tc.rect);
 }
 
+void tile_rects(bool enabled, const std::vector<float4>& bounds, const rrte_scene_ir* s, const rrte_render_params* p,
+                KParams& kk);
 void fill_tile_rects_uncached(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, KParams& kk) {
+    tile_rects(c->env_tile_cull, c->h_bounds, s, p, kk);
+}
+void tile_rects(bool enabled, const std::vector<float4>& bounds, const rrte_scene_ir* s, const rrte_render_params* p,
+                KParams& kk) {
     FrameCam& k = kk.cam[0];
     const uint32_t band_rows = kk.band_rows;
     k.tile_cull = 0;
@@ -922,8 +942,7 @@ void fill_tile_rects_uncached(const rrte_ctx* c, const rrte_scene_ir* s, const r
                (band_rows == 0 || band_rows % t == 0);
     };
     const uint32_t sh = fits(3) ? 3u : (fits(4) ? 4u : 0u);
-    if (!c->env_tile_cull || s->camera.projection != RRTE_PERSPECTIVE || sh == 0 ||
-        c->h_bounds.size() < s->num_prims)
+    if (!enabled || s->camera.projection != RRTE_PERSPECTIVE || sh == 0 || bounds.size() < s->num_prims)
         return;
     const uint32_t nbx = (p->width + (1u << sh) - 1) >> sh, nby = (p->height + (1u << sh) - 1) >> sh;
     const rrte_camera& cam = s->camera;
@@ -945,7 +964,7 @@ void fill_tile_rects_uncached(const rrte_ctx* c, const rrte_scene_ir* s, const r
     const uint32_t n = s->num_prims < 32u ? s->num_prims : 32u;
     const double margin = 2.0;
     for (uint32_t i = 0; i < n; ++i) {
-        const float4 b = c->h_bounds[i];
+        const float4 b = bounds[i];
         uint32_t rect = 0u | ((nbx - 1) << 8) | (0u << 16) | ((nby - 1) << 24);  // whole frame
         const double R = (double)b.w;
         const double w[3] = {(double)b.x - cam.position[0], (double)b.y - cam.position[1], (double)b.z - cam.position[2]};
@@ -985,14 +1004,95 @@ void fill_tile_rects_uncached(const rrte_ctx* c, const rrte_scene_ir* s, const r
     k.tile_cull = sh;
 }
 
-uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank) {
+uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank, uint32_t sky = 0u,
+                       uint32_t root_share = 1u) {
     if (nranks <= 1 || band_rows == 0) return height;
+    const BandMap m{band_rows, (uint32_t)nranks, sky, root_share};
     uint32_t nb = (height + band_rows - 1) / band_rows, rows = 0;
-    for (uint32_t b = (uint32_t)rank; b < nb; b += (uint32_t)nranks) {
+    for (uint32_t b = 0; b < nb; ++b) {
+        uint32_t lb = 0;
+        if (band_owner(m, b, lb) != (uint32_t)rank) continue;
         uint32_t r0 = b * band_rows, r1 = r0 + band_rows < height ? r0 + band_rows : height;
         rows += r1 - r0;
     }
     return rows;
+}
+
+// The band partition of a multi-GPU frame (BandMap, device_scene.hpp).  The leading "sky" bands --
+// rows above every object's silhouette, where every camera ray misses (the cheapest rows of the
+// frame) -- go to the root; the other bands go round robin, the root taking a share only when the
+// sky rows are fewer than a fair share (H / N).  The silhouette top: per object, the cone of
+// directions from the eye that meet its culling sphere, cut at 17 columns across the frame on the
+// image plane (a quadratic per column, double precision), minus one band of margin.  This decides
+// only WHICH rank renders a band -- never a pixel -- so the sampling need not be conservative.
+// Every rank computes the same partition from the same scene and camera (host arithmetic only).
+// RRTE_BAND_SKY=0: the plain interleave.
+BandMap band_layout(const rrte_camera& cam, const std::vector<float4>& bounds, uint32_t num_prims, uint32_t width,
+                    uint32_t height, uint32_t band_rows, int nranks, int root, bool enabled) {
+    BandMap m{band_rows, (uint32_t)std::max(nranks, 1), 0u, 1u};
+    if (!enabled || nranks <= 1 || root != 0 || band_rows == 0 || cam.projection != RRTE_PERSPECTIVE ||
+        bounds.size() < num_prims || num_prims == 0)
+        return m;
+    double q[4] = {cam.rotation[0], cam.rotation[1], cam.rotation[2], cam.rotation[3]};
+    const double qn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const double hh = std::tan(0.5 * (double)cam.fov), hw = (double)cam.aspect_ratio * hh;
+    if (!(qn > 0.0) || !std::isfinite(qn) || !(hh > 0.0) || !(hw > 0.0) || !std::isfinite(hh * hw)) return m;
+    for (double& v : q) v /= qn;
+    auto to_cam = [&](const double v[3], double out[3]) {  // the inverse rotation (as fill_tile_rects)
+        const double bx = -q[0], by = -q[1], bz = -q[2], w = q[3];
+        const double vb = v[0] * bx + v[1] * by + v[2] * bz, k0 = w * w - (bx * bx + by * by + bz * bz);
+        const double cx = by * v[2] - bz * v[1], cy = bz * v[0] - bx * v[2], cz = bx * v[1] - by * v[0];
+        out[0] = v[0] * k0 + 2.0 * bx * vb + 2.0 * w * cx;
+        out[1] = v[1] * k0 + 2.0 * by * vb + 2.0 * w * cy;
+        out[2] = v[2] * k0 + 2.0 * bz * vb + 2.0 * w * cz;
+    };
+    double top = std::numeric_limits<double>::infinity();  // topmost image row any object reaches
+    for (uint32_t i = 0; i < num_prims; ++i) {
+        const float4 b = bounds[i];
+        const double R = b.w;
+        const double w[3] = {(double)b.x - cam.position[0], (double)b.y - cam.position[1], (double)b.z - cam.position[2]};
+        double v[3];
+        to_cam(w, v);
+        const double D = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        if (!std::isfinite(R) || !std::isfinite(D) || D <= R * 1.0001) return m;  // unbounded / around the eye
+        const double u[3] = {v[0] / D, v[1] / D, v[2] / D}, cos2 = 1.0 - (R / D) * (R / D);
+        for (int col = 0; col <= 16; ++col) {
+            // image-plane point (px, s, -1): inside the cone iff d = u.p > 0 and d^2 >= cos2 |p|^2
+            const double px = (2.0 * col / 16.0 - 1.0) * hw, k = u[0] * px - u[2], mm = px * px + 1.0;
+            const double A = u[1] * u[1] - cos2, B = 2.0 * u[1] * k, C = k * k - cos2 * mm;
+            auto inside = [&](double s) { return u[1] * s + k > 0.0 && A * s * s + B * s + C >= -1e-12; };
+            double cand[3] = {hh, -std::numeric_limits<double>::infinity(), -std::numeric_limits<double>::infinity()};
+            const double disc = B * B - 4.0 * A * C;
+            if (A != 0.0 && disc >= 0.0) {
+                const double sq = std::sqrt(disc);
+                cand[1] = (-B + sq) / (2.0 * A);
+                cand[2] = (-B - sq) / (2.0 * A);
+            } else if (A == 0.0 && B != 0.0) {
+                cand[1] = -C / B;
+            }
+            std::sort(cand, cand + 3, [](double x, double y) { return x > y; });
+            for (double sv : cand) {
+                if (!(sv <= hh) || !(sv >= -hh) || !inside(sv)) continue;
+                top = std::min(top, (1.0 - sv / hh) * height * 0.5 - 0.5);  // image row of ndc_y = s / hh
+                break;
+            }
+        }
+    }
+    const double free_rows = top - band_rows;  // one band of margin
+    const uint32_t nb = (height + band_rows - 1) / band_rows;
+    uint32_t sky = free_rows > 0.0 ? (uint32_t)std::min<double>(std::floor(free_rows / band_rows), nb) : 0u;
+    if (sky >= nb) sky = 0;  // (nothing visible at all: the plain interleave)
+    m.sky = sky;
+    // The root's round-robin share: whichever choice gives the smaller busiest rank under a work model
+    // -- a sky row costs kSkyCost of an average row (a camera ray that misses: tile profiles put sky
+    // tiles at ~3 us against ~15 us on average), and the root spends kExpandCost of a frame's work on
+    // expanding the peers' RGB24 rows (the batched composition, ~3 of ~67 us per 1080p frame)
+    constexpr double kSkyCost = 0.2, kExpandCost = 0.04;
+    const double n = (double)nranks, fs = kSkyCost * sky * band_rows / height, rest = 1.0 - fs;
+    const double without = std::max(fs + kExpandCost * rest, rest / (n - 1.0));
+    const double with = std::max(fs + rest / n + kExpandCost * rest * (n - 1.0) / n, rest / n);
+    m.root_share = with <= without ? 1u : 0u;
+    return m;
 }
 
 // Shadow-ray culling (ray_kernels.hpp, shadow_cull) for LAMBERT_SHADOW frames: one lane per object,
@@ -1127,9 +1227,13 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
 }
 
 LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
-                       uint32_t internal_flags, uint32_t row0 = 0u) {
+                       uint32_t internal_flags, uint32_t row0 = 0u, const BandMap* bm = nullptr) {
     LaunchPlan L;
     L.k = make_params(c, s, p, rows);
+    if (bm && L.k.band_rows) {
+        L.k.sky_bands = bm->sky;
+        L.k.root_share = bm->root_share;
+    }
     L.k.row0 = row0;  // (image rows [row0, row0 + rows); band_rows == 0)
     L.k.flags |= internal_flags;
     L.mode = (int)p->mode;
@@ -1144,6 +1248,26 @@ LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_pa
     L.gy = (rows + 7) / 8;
     fill_tile_rects(c, s, p, L.k);
     return L;
+}
+
+// The band partition of one multi-GPU frame of this context (band_layout from the frame's camera-ray
+// tile rectangles; `p` with its band_rows set).
+BandMap frame_band_map(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root) {
+    auto& bc = c->band_cache;  // (the same camera, scene, size and rank count: the last answer)
+    if (bc.valid && bc.gen == c->scene_gen && bc.w == p->width && bc.h == p->height && bc.band == p->band_rows &&
+        bc.nranks == c->nranks && bc.root == root && !memcmp(&bc.cam, &s->camera, sizeof bc.cam))
+        return bc.m;
+    bc.m = band_layout(s->camera, c->h_bounds, s->num_prims, p->width, p->height, p->band_rows, c->nranks, root,
+                       c->env_band_sky);
+    bc.valid = true;
+    bc.gen = c->scene_gen;
+    bc.w = p->width;
+    bc.h = p->height;
+    bc.band = p->band_rows;
+    bc.nranks = c->nranks;
+    bc.root = root;
+    bc.cam = s->camera;
+    return bc.m;
 }
 
 // Measured-cost tile order (rrte_ctx::TileProfile, KParams::hot).
@@ -1397,9 +1521,9 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
 
 rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
                    uint32_t* d_rgba, float4* d_f32, hipStream_t st, uint32_t internal_flags = 0u, uint32_t row0 = 0u,
-                   int prof = 0) {
+                   int prof = 0, const BandMap* bm = nullptr) {
     if (rows == 0) return RRTE_OK;
-    LaunchPlan L = plan_launch(c, s, p, rows, internal_flags, row0);
+    LaunchPlan L = plan_launch(c, s, p, rows, internal_flags, row0, bm);
     L.prof = prof;
     return issue_launch(c, L, d_rgba, d_f32, st);
 }
@@ -1560,6 +1684,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_BATCH_SLABS"); g && *g)
         c->batch_slabs = std::max(1, std::min(rrte_ctx::kBatchSlabs, (int)strtol(g, nullptr, 0)));
     if (const char* g = getenv("RRTE_GATHER_SELF")) c->env_gather_self = g[0] == '1';
+    if (const char* g = getenv("RRTE_BAND_SKY")) c->env_band_sky = g[0] != '0';
     if (const char* g = getenv("RRTE_COMM_PRIORITY")) c->env_comm_priority = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
@@ -1702,16 +1827,18 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
     const int nr = c->nranks, rk = c->rank;
     uint32_t rows = p->height;
     rrte_render_params pe = *p;
+    BandMap bm{0u, 1u, 0u, 1u};
     if (c->emu_nranks > 1) {  // diagnostic: exactly one rank's share of a multi-GPU frame, packed
         c->nranks = c->emu_nranks;
         c->rank = c->emu_rank;
         pe.band_rows = p->band_rows ? p->band_rows : 16;
-        rows = rows_for_rank(p->height, pe.band_rows, c->nranks, c->rank);
+        bm = frame_band_map(c, s, &pe, 0);
+        rows = rows_for_rank(p->height, pe.band_rows, c->nranks, c->rank, bm.sky, bm.root_share);
     } else {
         c->nranks = 1;
         c->rank = 0;
     }
-    r = launch(c, s, &pe, rows, static_cast<uint32_t*>(d_rgba), static_cast<float4*>(d_f32), st);
+    r = launch(c, s, &pe, rows, static_cast<uint32_t*>(d_rgba), static_cast<float4*>(d_f32), st, 0u, 0u, 0, &bm);
     c->nranks = nr;
     c->rank = rk;
     if (r != RRTE_OK) return r;
@@ -1871,6 +1998,34 @@ uint32_t rrte_hip_band_rows_for_rank(uint32_t height, uint32_t band_rows, int nr
     return rows_for_rank(height, band_rows, nranks, rank);
 }
 
+rrte_status rrte_hip_band_layout(const rrte_scene_ir* s, const rrte_render_params* p, int nranks, int root,
+                                 uint32_t* sky_bands, uint32_t* root_share) {
+    if (!s || !p || !sky_bands || !root_share || nranks < 1 || root < 0 || root >= nranks) return RRTE_INVALID_ARG;
+    if ((s->num_prims && !s->prims) || (s->num_mesh_indices && !s->mesh_indices) ||
+        (s->num_mesh_vertices && !s->mesh_vertices))
+        return RRTE_INVALID_ARG;
+    rrte_render_params pp = *p;
+    if (!pp.band_rows) pp.band_rows = 16;
+    std::vector<DPrim> prims;
+    std::vector<DMaterial> mats;
+    std::vector<DLight> lights;
+    std::vector<float4> bounds;
+    lower_scene(s, prims, mats, lights, &bounds);
+    MeshData md;
+    build_mesh_bvhs(s, prims.data(), md, bounds.data());
+    const char* g = getenv("RRTE_BAND_SKY");
+    const BandMap m = band_layout(s->camera, bounds, s->num_prims, pp.width, pp.height, pp.band_rows, nranks, root,
+                                  !(g && g[0] == '0'));
+    *sky_bands = m.sky;
+    *root_share = m.root_share;
+    return RRTE_OK;
+}
+
+uint32_t rrte_hip_band_rows_for_rank_ex(uint32_t height, uint32_t band_rows, int nranks, int rank, uint32_t sky_bands,
+                                        uint32_t root_share) {
+    return rows_for_rank(height, band_rows, nranks, rank, sky_bands, root_share ? 1u : 0u);
+}
+
 rrte_status rrte_hip_comm_unique_id(uint8_t out_id[RRTE_UNIQUE_ID_BYTES]) {
     if (!out_id) return RRTE_INVALID_ARG;
     static_assert(sizeof(ncclUniqueId) == RRTE_UNIQUE_ID_BYTES, "unique id size");
@@ -1955,21 +2110,20 @@ bool slab_rgb24(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_par
 // frames in the same order), so the collective matches.
 // De-interleave `n` gathered frames (ray_kernels.hpp deinterleave_batch_kernel) on `st`.
 static rrte_status deinterleave(rrte_ctx* c, hipStream_t st, const uint8_t* gathered, const DeinterleaveTargets& t,
-                                uint32_t n, uint32_t width, uint32_t height, uint32_t band, bool rgb24,
+                                uint32_t n, uint32_t width, uint32_t height, const BandMap& bm, bool rgb24,
                                 size_t rank_stride, size_t frame_stride, uint32_t skip_rank = ~0u) {
     bool vec4 = width % 4u == 0;
     for (uint32_t j = 0; j < n; ++j) vec4 = vec4 && reinterpret_cast<uintptr_t>(t.full[j]) % 16u == 0;
     const uint32_t per = vec4 ? 1024u : 256u;  // pixels one workgroup moves per pass
     const dim3 dg(std::min((width + per - 1) / per, 8u), height, n), db(256);
-    const uint32_t nr = (uint32_t)c->nranks;
     if (rgb24 && vec4)
-        hipLaunchKernelGGL((deinterleave_batch_kernel<true, true>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride, skip_rank);
+        hipLaunchKernelGGL((deinterleave_batch_kernel<true, true>), dg, db, 0, st, gathered, t, width, bm, rank_stride, frame_stride, skip_rank);
     else if (rgb24)
-        hipLaunchKernelGGL((deinterleave_batch_kernel<true, false>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride, skip_rank);
+        hipLaunchKernelGGL((deinterleave_batch_kernel<true, false>), dg, db, 0, st, gathered, t, width, bm, rank_stride, frame_stride, skip_rank);
     else if (vec4)
-        hipLaunchKernelGGL((deinterleave_batch_kernel<false, true>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride, skip_rank);
+        hipLaunchKernelGGL((deinterleave_batch_kernel<false, true>), dg, db, 0, st, gathered, t, width, bm, rank_stride, frame_stride, skip_rank);
     else
-        hipLaunchKernelGGL((deinterleave_batch_kernel<false, false>), dg, db, 0, st, gathered, t, width, band, nr, rank_stride, frame_stride, skip_rank);
+        hipLaunchKernelGGL((deinterleave_batch_kernel<false, false>), dg, db, 0, st, gathered, t, width, bm, rank_stride, frame_stride, skip_rank);
     HIPCHK(c, hipGetLastError());
     return RRTE_OK;
 }
@@ -2184,7 +2338,7 @@ static rrte_status flush_batch(rrte_ctx* c) {
         if (c->rank == b.root && !(c->env_diag_skip & 2u) && (c->nranks > 1 || !b.in_place)) {
             DeinterleaveTargets t{};
             for (uint32_t j = 0; j < b.n; ++j) t.full[j] = b.full[j];
-            if ((r = deinterleave(c, c->comm_stream, c->d_brecv[k], t, b.n, b.width, b.height, b.band, b.rgb24, count,
+            if ((r = deinterleave(c, c->comm_stream, c->d_brecv[k], t, b.n, b.width, b.height, b.bm, b.rgb24, count,
                                   b.slice, b.in_place ? (uint32_t)b.root : ~0u)) != RRTE_OK)
                 return r;
         }
@@ -2220,8 +2374,10 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
     const uint32_t band = p->band_rows ? p->band_rows : 16;
     rrte_render_params pp = *p;
     pp.band_rows = band;
-    const uint32_t rows = rows_for_rank(p->height, band, c->nranks, c->rank);
-    const uint32_t cap = rows_for_rank(p->height, band, c->nranks, 0);  // rank 0 owns the most rows
+    const BandMap bm = c->nranks > 1 ? frame_band_map(c, s, &pp, root) : BandMap{band, 1u, 0u, 1u};
+    const uint32_t rows = rows_for_rank(p->height, band, c->nranks, c->rank, bm.sky, bm.root_share);
+    uint32_t cap = 0;  // slab rows: the most any rank owns
+    for (int q = 0; q < c->nranks; ++q) cap = std::max(cap, rows_for_rank(p->height, band, c->nranks, q, bm.sky, bm.root_share));
     const bool rgb24 = slab_rgb24(c, s, p);
     // bytes per rank slot, 256-B aligned so every rank's send buffer starts aligned
     const size_t slice = ((size_t)cap * p->width * (rgb24 ? 3u : 4u) + 255u) & ~(size_t)255u;
@@ -2253,7 +2409,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             for (int i = 0; i < rrte_ctx::kMaxBatch; ++i)
                 HIPCHK(c, hipEventCreateWithFlags(&b.ev_src[i], hipEventDisableTiming));
         }
-        LaunchPlan L = plan_launch(c, s, &pp, rows, kflags);
+        LaunchPlan L = plan_launch(c, s, &pp, rows, kflags, 0u, &bm);
         // a frame of another size, band, root, slab format or render setup closes the open batch
         // (the cameras and tile rectangles are per frame; everything before KParams::nframes is not)
         if (b.n && (b.width != p->width || b.height != p->height || b.band != band || b.root != root ||
@@ -2269,6 +2425,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             b.root = root;
             b.rgb24 = rgb24;
             b.slice = slice;
+            b.bm = bm;
             b.plan = L;
             b.in_place = c->rank == root && !c->env_gather_self;
             // every rank holds a receive slab too (the root's is the only one written)
@@ -2313,7 +2470,8 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         if (c->slab_stream[slot] && c->slab_stream[slot] != st)
             HIPCHK(c, hipStreamWaitEvent(st, c->ev_gath[slot], 0));
         hs.lap(2);
-        if ((r = launch(c, s, &pp, rows, reinterpret_cast<uint32_t*>(mine), nullptr, st, kflags)) != RRTE_OK) return r;
+        if ((r = launch(c, s, &pp, rows, reinterpret_cast<uint32_t*>(mine), nullptr, st, kflags, 0u, 0, &bm)) != RRTE_OK)
+            return r;
         hs.lap(3);
         if (timing) HIPCHK(c, hipEventRecord(c->ev1, st));
         // gathers on one communicator must run in the same order on every rank: a frame on another
@@ -2330,7 +2488,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         if (c->rank == root) {
             DeinterleaveTargets t{};
             t.full[0] = static_cast<uint32_t*>(d_full);
-            if ((r = deinterleave(c, st, slab, t, 1, p->width, p->height, band, rgb24, slice, 0)) != RRTE_OK)
+            if ((r = deinterleave(c, st, slab, t, 1, p->width, p->height, bm, rgb24, slice, 0)) != RRTE_OK)
                 return comm_abort(c, ("de-interleave failed: " + c->err).c_str());
         }
         hs.lap(6);

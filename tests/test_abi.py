@@ -98,3 +98,58 @@ def test_fpcheck_rejects_bad_ranges():
     assert lib.rrte_hip_fpcheck(0, -1, 0, 1, C.byref(out)) == 1
     assert lib.rrte_hip_fpcheck(0, abi.FPCHECK_SQRT, 5, 4, C.byref(out)) == 1
     assert lib.rrte_hip_fpcheck(0, abi.FPCHECK_SQRT, 0, 1, None) == 1
+
+
+def _band_of_local(rank, lb, n, sky, rs):
+    """Mirror of device_scene.hpp band_of_local."""
+    L = n - 1 + rs
+    if rank == 0:
+        return lb if lb < sky else sky + (lb - sky) * L
+    return sky + (rank - 1 + rs) + lb * L
+
+
+@pytest.mark.parametrize("H,band,n", [(1080, 16, 2), (1080, 16, 8), (2160, 16, 8), (1000, 16, 3), (7, 16, 4),
+                                      (480, 16, 8), (1080, 8, 5)])
+@pytest.mark.parametrize("sky,rs", [(0, 1), (3, 1), (16, 0), (16, 1), (40, 0)])
+def test_sky_band_partition_covers_every_row_once(H, band, n, sky, rs):
+    """rrte_hip_band_rows_for_rank_ex and the device mapping (band_of_local) for a partition with sky
+    bands on rank 0: every image row exactly once, packed in image order per rank."""
+    lib = abi.load()
+    nb = (H + band - 1) // band
+    sky = min(sky, nb - 1)
+    if rs == 0 and sky == 0:
+        return  # (not a layout band_layout produces: the root would own nothing)
+    rows = [lib.rrte_hip_band_rows_for_rank_ex(H, band, n, r, sky, rs) for r in range(n)]
+    assert sum(rows) == H
+    seen = []
+    for r in range(n):
+        prev = -1
+        for lr in range(rows[r]):
+            b, w = divmod(lr, band)
+            y = _band_of_local(r, b, n, sky, rs) * band + w
+            assert y > prev  # packed in image order
+            prev = y
+            seen.append(y)
+    assert sorted(seen) == list(range(H))
+
+
+def test_band_layout_of_the_showcase():
+    """The showcase camera sees sky above every object: the leading bands go to rank 0; none with one
+    rank, none with RRTE_BAND_SKY=0 (the plain interleave), none for the all-covering ground views."""
+    from rrte_amd import LoweredScene, scenes
+    lib = abi.load()
+    objs, lights, cam, cfg = scenes.sdf_showcase(1920, 1080)
+    cfg.band_rows = 16
+    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    sky, rs = C.c_uint32(), C.c_uint32()
+
+    def layout(n):
+        assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), n, 0, C.byref(sky), C.byref(rs)) == abi.RRTE_OK
+        return sky.value, rs.value
+    s8, rs8 = layout(8)
+    assert 8 <= s8 < 34 and rs8 == 0  # ~a quarter of the rows is sky; at 8 ranks the root keeps to it
+    assert layout(2)[1] == 1  # at 2 ranks the root also takes a round-robin share
+    assert layout(1) == (0, 1)
+    assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), 8, 3, C.byref(sky), C.byref(rs)) == abi.RRTE_OK
+    assert (sky.value, rs.value) == (0, 1)  # a root other than rank 0: the plain interleave
+    assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), 0, 0, C.byref(sky), C.byref(rs)) == abi.RRTE_INVALID_ARG

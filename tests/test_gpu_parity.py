@@ -311,10 +311,8 @@ def test_camera_tile_culling_with_band_mapping(band, jit, monkeypatch):
         ctxs[tc] = Context(0, jit=jit)
     monkeypatch.delenv("RRTE_EMULATE_RANK")
     lib = abi.load()
+    from test_gpu_4k import band_owner
     for w, h in ((131, 77), (200, 112), (2101, 40)):  # 8x8 tiles; 16x16 blocks past 2048 pixels
-        rows = lib.rrte_hip_band_rows_for_rank(h, band, nranks, rank)
-        img_rows = [y for y in range(h) if (y // band) % nranks == rank]  # packed in image order
-        assert len(img_rows) == rows
         for pos, tgt, fov in poses:
             objs, lights, _, cfg = scenes.SCENES[name](w, h, mode="lambert_shadow")
             cfg.band_rows = band
@@ -325,6 +323,12 @@ def test_camera_tile_culling_with_band_mapping(band, jit, monkeypatch):
             sc = LoweredScene(objs, lights, cam)
             prm = cfg.lower()
             prm.flags |= abi.FLAG_F32_LINEAR
+            # this pose's band partition (sky bands on rank 0, the rest round robin)
+            sky, rs = C.c_uint32(), C.c_uint32()
+            assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), nranks, 0, C.byref(sky), C.byref(rs)) == 0
+            rows = lib.rrte_hip_band_rows_for_rank_ex(h, band, nranks, rank, sky.value, rs.value)
+            img_rows = [y for y in range(h) if band_owner(y // band, nranks, sky.value, rs.value) == rank]
+            assert len(img_rows) == rows
             out = {}
             for tc, ctx in ctxs.items():
                 f32 = torch.zeros(rows * w * 4, dtype=torch.float32, device="cuda")
