@@ -414,15 +414,18 @@ rrte_status rrte_hip_flush(rrte_ctx* ctx);
 /* Rows owned by `rank` under the plain band interleave (band b on rank b % nranks). */
 uint32_t rrte_hip_band_rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank);
 /* The band partition a multi-GPU frame of `scene` / `params` uses (DESIGN.md §5 "Band partition"): the
- * first *sky_bands bands (bands no object can reach, from the camera-ray tile rectangles: every camera
- * ray there misses) belong to rank 0, and the remaining bands go round robin over the ranks, rank 0
- * included only when *root_share is 1.  Band b then belongs to: b < sky -> 0; else with q = b - sky,
- * L = nranks - 1 + root_share: root_share ? q % L : 1 + q % L.  Computed identically on every rank;
- * host only.  (env RRTE_BAND_SKY=0: sky 0, root_share 1 -- the plain interleave.)  Rank 0 must be
- * the root for a sky share (otherwise the plain interleave). */
+ * first *sky_bands bands (bands no object can reach, judged from the camera and the objects' culling
+ * spheres: every camera ray there misses) belong to rank 0; the remaining bands go round robin in
+ * cycles of L bands.  With k = *root_share in [1, 8] a cycle is one band for rank 0, then k bands for
+ * every peer (L = 1 + (nranks - 1) k); with k = 0 rank 0 takes none (L = nranks - 1).  Band b then
+ * belongs to: b < sky -> 0; else with q = b - sky, s = q % L: (k && s == 0) -> 0, otherwise
+ * 1 + (s - (k ? 1 : 0)) % (nranks - 1).  k is chosen by a work model (sky rows are cheap, the root
+ * expands the peers' rows).  Computed identically on every rank; host only.  (env RRTE_BAND_SKY=0:
+ * sky 0, root_share 1 -- the plain interleave.)  Rank 0 must be the root for a root-biased partition
+ * (otherwise the plain interleave). */
 rrte_status rrte_hip_band_layout(const rrte_scene_ir* scene, const rrte_render_params* params, int nranks, int root,
                                  uint32_t* sky_bands, uint32_t* root_share);
-/* Rows owned by `rank` under that partition, in the order they are packed. */
+/* Rows owned by `rank` under that partition, in the order they are packed (0 for root_share > 8). */
 uint32_t rrte_hip_band_rows_for_rank_ex(uint32_t height, uint32_t band_rows, int nranks, int rank, uint32_t sky_bands,
                                         uint32_t root_share);
 

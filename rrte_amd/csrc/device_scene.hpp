@@ -88,17 +88,24 @@ __host__ __device__ constexpr uint32_t hot_y(uint32_t h) { return h >> 16; }
 
 // Multi-GPU row-band partition (DESIGN.md §5 "Band partition").  The image is cut into
 // bands of `band_rows` rows.  The first `sky` bands -- rows no object can reach, judged on the host
-// from the camera-ray tile rectangles, so every camera ray there misses (the cheapest rows of the
-// frame) -- belong to rank 0 (the root: its rows never cross a link); the remaining bands go round
-// robin over the ranks, the root included only when `root_share` is 1.  sky = 0, root_share = 1 is
-// the plain interleave band % nranks == rank.  Which rank renders a band never changes a pixel.
+// from the camera and the objects' culling spheres, so every camera ray there misses (the cheapest
+// rows of the frame) -- belong to rank 0 (the root: its rows never cross a link).  The remaining
+// bands go round robin in cycles: with root_share = k >= 1 a cycle is one band for the root, then k
+// bands for every peer (peer order repeated k times); with root_share = 0 the root takes none.
+// sky = 0, root_share = 1 is the plain interleave band % nranks == rank.  A larger k frees the root
+// for the expansion of the peers' rows it does per frame.  Which rank renders a band never changes a
+// pixel.
 struct BandMap {
     uint32_t band_rows, nranks, sky, root_share;
 };
+__host__ __device__ constexpr uint32_t band_cycle(const BandMap& m) {  // bands per round-robin cycle
+    return (m.root_share ? 1u : 0u) + (m.nranks - 1u) * (m.root_share ? m.root_share : 1u);
+}
 // The image band of `rank`'s local band lb.
 __host__ __device__ constexpr uint32_t band_of_local(const BandMap& m, uint32_t rank, uint32_t lb) {
-    const uint32_t L = m.nranks - 1u + m.root_share;  // bands per round-robin cycle
-    return rank == 0u ? (lb < m.sky ? lb : m.sky + (lb - m.sky) * L) : m.sky + (rank - 1u + m.root_share) + lb * L;
+    const uint32_t L = band_cycle(m), rs = m.root_share ? 1u : 0u, k = m.root_share ? m.root_share : 1u;
+    return rank == 0u ? (lb < m.sky ? lb : m.sky + (lb - m.sky) * L)
+                      : m.sky + (lb / k) * L + rs + (rank - 1u) + (lb % k) * (m.nranks - 1u);
 }
 // The rank owning image band b and its local band index there.
 __host__ __device__ constexpr uint32_t band_owner(const BandMap& m, uint32_t b, uint32_t& lb) {
@@ -106,10 +113,15 @@ __host__ __device__ constexpr uint32_t band_owner(const BandMap& m, uint32_t b, 
         lb = b;
         return 0u;
     }
-    const uint32_t L = m.nranks - 1u + m.root_share, q = b - m.sky, slot = q % L;
-    const uint32_t owner = m.root_share ? slot : slot + 1u;
-    lb = owner == 0u ? m.sky + q / L : q / L;
-    return owner;
+    const uint32_t L = band_cycle(m), rs = m.root_share ? 1u : 0u, k = m.root_share ? m.root_share : 1u;
+    const uint32_t q = b - m.sky, cyc = q / L, slot = q % L;
+    if (rs && slot == 0u) {
+        lb = m.sky + cyc;
+        return 0u;
+    }
+    const uint32_t s = slot - rs;
+    lb = cyc * k + s / (m.nranks - 1u);
+    return 1u + s % (m.nranks - 1u);
 }
 
 // Per-launch constants, passed by value (kernel arguments land in SGPRs).

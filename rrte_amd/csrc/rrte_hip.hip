@@ -286,9 +286,10 @@ struct rrte_ctx {
         bool valid = false;
         uint64_t gen = 0;
         uint32_t w = 0, h = 0, band = 0;
-        int nranks = 0, root = 0;
+        int nranks = 0, root = 0, rank = 0;
         rrte_camera cam{};
         BandMap m{};
+        uint32_t rows = 0, cap = 0;  // this rank's rows; the most rows any rank owns (slab rows)
     } band_cache;
     // camera-ray tile rectangles of the last camera (fill_tile_rects)
     struct {
@@ -1004,6 +1005,8 @@ void tile_rects(bool enabled, const std::vector<float4>& bounds, const rrte_scen
     k.tile_cull = sh;
 }
 
+constexpr uint32_t kMaxRootShare = 8u;  // largest root_share (peer bands per root band) band_layout picks
+
 uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank, uint32_t sky = 0u,
                        uint32_t root_share = 1u) {
     if (nranks <= 1 || band_rows == 0) return height;
@@ -1018,25 +1021,14 @@ uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank
     return rows;
 }
 
-// The band partition of a multi-GPU frame (BandMap, device_scene.hpp).  The leading "sky" bands --
-// rows above every object's silhouette, where every camera ray misses (the cheapest rows of the
-// frame) -- go to the root; the other bands go round robin, the root taking a share only when the
-// sky rows are fewer than a fair share (H / N).  The silhouette top: per object, the cone of
-// directions from the eye that meet its culling sphere, cut at 17 columns across the frame on the
-// image plane (a quadratic per column, double precision), minus one band of margin.  This decides
-// only WHICH rank renders a band -- never a pixel -- so the sampling need not be conservative.
-// Every rank computes the same partition from the same scene and camera (host arithmetic only).
-// RRTE_BAND_SKY=0: the plain interleave.
-BandMap band_layout(const rrte_camera& cam, const std::vector<float4>& bounds, uint32_t num_prims, uint32_t width,
-                    uint32_t height, uint32_t band_rows, int nranks, int root, bool enabled) {
-    BandMap m{band_rows, (uint32_t)std::max(nranks, 1), 0u, 1u};
-    if (!enabled || nranks <= 1 || root != 0 || band_rows == 0 || cam.projection != RRTE_PERSPECTIVE ||
-        bounds.size() < num_prims || num_prims == 0)
-        return m;
+// The number of leading bands no object reaches (band_layout); 0 when it cannot be judged.
+uint32_t sky_band_count(const rrte_camera& cam, const std::vector<float4>& bounds, uint32_t num_prims,
+                        uint32_t height, uint32_t band_rows) {
+    if (cam.projection != RRTE_PERSPECTIVE || bounds.size() < num_prims || num_prims == 0) return 0u;
     double q[4] = {cam.rotation[0], cam.rotation[1], cam.rotation[2], cam.rotation[3]};
     const double qn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
     const double hh = std::tan(0.5 * (double)cam.fov), hw = (double)cam.aspect_ratio * hh;
-    if (!(qn > 0.0) || !std::isfinite(qn) || !(hh > 0.0) || !(hw > 0.0) || !std::isfinite(hh * hw)) return m;
+    if (!(qn > 0.0) || !std::isfinite(qn) || !(hh > 0.0) || !(hw > 0.0) || !std::isfinite(hh * hw)) return 0u;
     for (double& v : q) v /= qn;
     auto to_cam = [&](const double v[3], double out[3]) {  // the inverse rotation (as fill_tile_rects)
         const double bx = -q[0], by = -q[1], bz = -q[2], w = q[3];
@@ -1054,7 +1046,7 @@ BandMap band_layout(const rrte_camera& cam, const std::vector<float4>& bounds, u
         double v[3];
         to_cam(w, v);
         const double D = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-        if (!std::isfinite(R) || !std::isfinite(D) || D <= R * 1.0001) return m;  // unbounded / around the eye
+        if (!std::isfinite(R) || !std::isfinite(D) || D <= R * 1.0001) return 0u;  // unbounded / around the eye
         const double u[3] = {v[0] / D, v[1] / D, v[2] / D}, cos2 = 1.0 - (R / D) * (R / D);
         for (int col = 0; col <= 16; ++col) {
             // image-plane point (px, s, -1): inside the cone iff d = u.p > 0 and d^2 >= cos2 |p|^2
@@ -1081,19 +1073,39 @@ BandMap band_layout(const rrte_camera& cam, const std::vector<float4>& bounds, u
     const double free_rows = top - band_rows;  // one band of margin
     const uint32_t nb = (height + band_rows - 1) / band_rows;
     uint32_t sky = free_rows > 0.0 ? (uint32_t)std::min<double>(std::floor(free_rows / band_rows), nb) : 0u;
-    if (sky >= nb) sky = 0;  // (nothing visible at all: the plain interleave)
-    m.sky = sky;
-    // The root's round-robin share: whichever choice gives the smaller busiest rank under a work model
-    // -- a sky row costs kSkyCost of an average row (a camera ray that misses: tile profiles put sky
-    // tiles at ~3 us against ~15 us on average), and the root spends kExpandCost of a frame's work on
-    // expanding the peers' RGB24 rows (the batched composition, ~3 of ~67 us per 1080p frame)
+    return sky >= nb ? 0u : sky;  // (nothing visible at all: the plain interleave)
+}
+
+// The band partition of a multi-GPU frame (BandMap, device_scene.hpp).  The leading "sky" bands --
+// rows above every object's silhouette, where every camera ray misses (the cheapest rows of the
+// frame) -- go to the root; the other bands go round robin, the root taking one band per k of every
+// peer's (root_share = k; 0 = none), k chosen by a work model so the busiest rank is least busy.
+// The silhouette top: per object, the cone of directions from the eye that meet its culling sphere,
+// cut at 17 columns across the frame on the image plane (a quadratic per column, double precision),
+// minus one band of margin.  This decides only WHICH rank renders a band -- never a pixel -- so the
+// sampling need not be conservative.  Every rank computes the same partition from the same scene and
+// camera (host arithmetic only).  RRTE_BAND_SKY=0: the plain interleave (sky 0, k 1).
+BandMap band_layout(const rrte_camera& cam, const std::vector<float4>& bounds, uint32_t num_prims, uint32_t width,
+                    uint32_t height, uint32_t band_rows, int nranks, int root, bool enabled) {
+    BandMap m{band_rows, (uint32_t)std::max(nranks, 1), 0u, 1u};
+    if (!enabled || nranks <= 1 || root != 0 || band_rows == 0) return m;
+    m.sky = sky_band_count(cam, bounds, num_prims, height, band_rows);
+    // The root's round-robin share: the k giving the smallest busiest rank under a work model -- a sky
+    // row costs kSkyCost of an average row (a camera ray that misses: tile profiles put sky tiles at
+    // ~3 us against ~15 us on average), and the root spends kExpandCost of a frame's work expanding
+    // the peers' RGB24 rows (the batched composition, ~3 of ~67 us per 1080p frame)
     constexpr double kSkyCost = 0.2, kExpandCost = 0.04;
-    const double n = (double)nranks, fs = kSkyCost * sky * band_rows / height, rest = 1.0 - fs;
-    const double without = std::max(fs + kExpandCost * rest, rest / (n - 1.0));
-    const double with = std::max(fs + rest / n + kExpandCost * rest * (n - 1.0) / n, rest / n);
-    m.root_share = with <= without ? 1u : 0u;
+    const double n = (double)nranks, fs = kSkyCost * m.sky * band_rows / height, rest = 1.0 - fs;
+    double best = std::max(fs + kExpandCost * rest, rest / (n - 1.0));  // k = 0
+    m.root_share = 0u;
+    for (uint32_t k = 1; k <= kMaxRootShare; ++k) {
+        const double L = 1.0 + (n - 1.0) * k;
+        const double load = std::max(fs + rest / L + kExpandCost * rest * (1.0 - 1.0 / L), rest * k / L);
+        if (load < best - 1e-9) best = load, m.root_share = k;
+    }
     return m;
 }
+
 
 // Shadow-ray culling (ray_kernels.hpp, shadow_cull) for LAMBERT_SHADOW frames: one lane per object,
 // so scenes of <= 64 objects; it pays where an occlusion test is expensive (sphere-traced SDF
@@ -1252,21 +1264,32 @@ LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_pa
 
 // The band partition of one multi-GPU frame of this context (band_layout from the frame's camera-ray
 // tile rectangles; `p` with its band_rows set).
-BandMap frame_band_map(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root) {
-    auto& bc = c->band_cache;  // (the same camera, scene, size and rank count: the last answer)
-    if (bc.valid && bc.gen == c->scene_gen && bc.w == p->width && bc.h == p->height && bc.band == p->band_rows &&
-        bc.nranks == c->nranks && bc.root == root && !memcmp(&bc.cam, &s->camera, sizeof bc.cam))
-        return bc.m;
-    bc.m = band_layout(s->camera, c->h_bounds, s->num_prims, p->width, p->height, p->band_rows, c->nranks, root,
-                       c->env_band_sky);
-    bc.valid = true;
-    bc.gen = c->scene_gen;
-    bc.w = p->width;
-    bc.h = p->height;
-    bc.band = p->band_rows;
-    bc.nranks = c->nranks;
-    bc.root = root;
-    bc.cam = s->camera;
+// The band partition of a multi-GPU frame, this rank's rows under it and the slab rows (the most any
+// rank owns); the last answer is kept (the same camera, scene, size, rank and rank count)
+const BandMap& frame_band_map(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
+                              uint32_t* rows = nullptr, uint32_t* cap = nullptr) {
+    auto& bc = c->band_cache;
+    if (!(bc.valid && bc.gen == c->scene_gen && bc.w == p->width && bc.h == p->height && bc.band == p->band_rows &&
+          bc.nranks == c->nranks && bc.root == root && bc.rank == c->rank &&
+          !memcmp(&bc.cam, &s->camera, sizeof bc.cam))) {
+        bc.m = band_layout(s->camera, c->h_bounds, s->num_prims, p->width, p->height, p->band_rows, c->nranks, root,
+                           c->env_band_sky);
+        bc.valid = true;
+        bc.gen = c->scene_gen;
+        bc.w = p->width;
+        bc.h = p->height;
+        bc.band = p->band_rows;
+        bc.nranks = c->nranks;
+        bc.root = root;
+        bc.rank = c->rank;
+        bc.cam = s->camera;
+        bc.rows = rows_for_rank(p->height, p->band_rows, c->nranks, c->rank, bc.m.sky, bc.m.root_share);
+        bc.cap = 0;
+        for (int q = 0; q < c->nranks; ++q)
+            bc.cap = std::max(bc.cap, rows_for_rank(p->height, p->band_rows, c->nranks, q, bc.m.sky, bc.m.root_share));
+    }
+    if (rows) *rows = bc.rows;
+    if (cap) *cap = bc.cap;
     return bc.m;
 }
 
@@ -1832,8 +1855,7 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
         c->nranks = c->emu_nranks;
         c->rank = c->emu_rank;
         pe.band_rows = p->band_rows ? p->band_rows : 16;
-        bm = frame_band_map(c, s, &pe, 0);
-        rows = rows_for_rank(p->height, pe.band_rows, c->nranks, c->rank, bm.sky, bm.root_share);
+        bm = frame_band_map(c, s, &pe, 0, &rows);
     } else {
         c->nranks = 1;
         c->rank = 0;
@@ -2023,7 +2045,8 @@ rrte_status rrte_hip_band_layout(const rrte_scene_ir* s, const rrte_render_param
 
 uint32_t rrte_hip_band_rows_for_rank_ex(uint32_t height, uint32_t band_rows, int nranks, int rank, uint32_t sky_bands,
                                         uint32_t root_share) {
-    return rows_for_rank(height, band_rows, nranks, rank, sky_bands, root_share ? 1u : 0u);
+    if (root_share > kMaxRootShare) return 0u;  // (outside the documented range)
+    return rows_for_rank(height, band_rows, nranks, rank, sky_bands, root_share);
 }
 
 rrte_status rrte_hip_comm_unique_id(uint8_t out_id[RRTE_UNIQUE_ID_BYTES]) {
@@ -2374,10 +2397,8 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
     const uint32_t band = p->band_rows ? p->band_rows : 16;
     rrte_render_params pp = *p;
     pp.band_rows = band;
-    const BandMap bm = c->nranks > 1 ? frame_band_map(c, s, &pp, root) : BandMap{band, 1u, 0u, 1u};
-    const uint32_t rows = rows_for_rank(p->height, band, c->nranks, c->rank, bm.sky, bm.root_share);
-    uint32_t cap = 0;  // slab rows: the most any rank owns
-    for (int q = 0; q < c->nranks; ++q) cap = std::max(cap, rows_for_rank(p->height, band, c->nranks, q, bm.sky, bm.root_share));
+    uint32_t rows = p->height, cap = p->height;  // this rank's rows; slab rows (the most any rank owns)
+    const BandMap bm = c->nranks > 1 ? frame_band_map(c, s, &pp, root, &rows, &cap) : BandMap{band, 1u, 0u, 1u};
     const bool rgb24 = slab_rgb24(c, s, p);
     // bytes per rank slot, 256-B aligned so every rank's send buffer starts aligned
     const size_t slice = ((size_t)cap * p->width * (rgb24 ? 3u : 4u) + 255u) & ~(size_t)255u;

@@ -101,16 +101,17 @@ def test_fpcheck_rejects_bad_ranges():
 
 
 def _band_of_local(rank, lb, n, sky, rs):
-    """Mirror of device_scene.hpp band_of_local."""
-    L = n - 1 + rs
+    """Mirror of device_scene.hpp band_of_local (rs = root_share k: one root band per k of every peer's)."""
+    L = 1 + (n - 1) * rs if rs else n - 1
     if rank == 0:
         return lb if lb < sky else sky + (lb - sky) * L
-    return sky + (rank - 1 + rs) + lb * L
+    k = rs or 1
+    return sky + (lb // k) * L + (1 if rs else 0) + (rank - 1) + (lb % k) * (n - 1)
 
 
 @pytest.mark.parametrize("H,band,n", [(1080, 16, 2), (1080, 16, 8), (2160, 16, 8), (1000, 16, 3), (7, 16, 4),
                                       (480, 16, 8), (1080, 8, 5)])
-@pytest.mark.parametrize("sky,rs", [(0, 1), (3, 1), (16, 0), (16, 1), (40, 0)])
+@pytest.mark.parametrize("sky,rs", [(0, 1), (3, 1), (16, 0), (16, 1), (40, 0), (0, 2), (12, 3), (5, 8)])
 def test_sky_band_partition_covers_every_row_once(H, band, n, sky, rs):
     """rrte_hip_band_rows_for_rank_ex and the device mapping (band_of_local) for a partition with sky
     bands on rank 0: every image row exactly once, packed in image order per rank."""
@@ -147,9 +148,10 @@ def test_band_layout_of_the_showcase():
         assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), n, 0, C.byref(sky), C.byref(rs)) == abi.RRTE_OK
         return sky.value, rs.value
     s8, rs8 = layout(8)
-    assert 8 <= s8 < 34 and rs8 == 0  # ~a quarter of the rows is sky; at 8 ranks the root keeps to it
+    assert 8 <= s8 < 34 and 2 <= rs8 <= 8  # ~a quarter of the rows is sky; at 8 ranks a small root share
     assert layout(2)[1] == 1  # at 2 ranks the root also takes a round-robin share
     assert layout(1) == (0, 1)
     assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), 8, 3, C.byref(sky), C.byref(rs)) == abi.RRTE_OK
     assert (sky.value, rs.value) == (0, 1)  # a root other than rank 0: the plain interleave
     assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), 0, 0, C.byref(sky), C.byref(rs)) == abi.RRTE_INVALID_ARG
+    assert lib.rrte_hip_band_rows_for_rank_ex(1080, 16, 8, 1, 0, 9) == 0  # root_share beyond 8: rejected

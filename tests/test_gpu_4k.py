@@ -55,8 +55,12 @@ def band_owner(b, n, sky, root_share):
     """The rank owning image band b (include/rrte_hip.h rrte_hip_band_layout)."""
     if b < sky or n == 1:
         return 0
-    q, L = b - sky, n - 1 + root_share
-    return q % L if root_share else 1 + q % L
+    k = root_share
+    L = (1 + (n - 1) * k) if k else n - 1
+    s = (b - sky) % L
+    if k and s == 0:
+        return 0
+    return 1 + (s - (1 if k else 0)) % (n - 1)
 
 
 @pytest.mark.parametrize("sky_on", ["1", "0"])
