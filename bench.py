@@ -388,9 +388,10 @@ def main():
     timed_frames = [f.cpu().numpy().view(np.uint8).copy() for f in fulls[:min(F, args.steps)]] if rank == 0 else []
     rows = H
     if dist_on:  # this rank's rows under the frame's band partition (sky bands on the root, the rest round robin)
-        sky, rs = C.c_uint32(), C.c_uint32()
-        ctx.check(lib.rrte_hip_band_layout(scene.ref(), C.byref(prm), world, 0, C.byref(sky), C.byref(rs)))
-        rows = lib.rrte_hip_band_rows_for_rank_ex(H, args.band_rows, world, rank, sky.value, rs.value)
+        sky, rb, pb = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        ctx.check(lib.rrte_hip_band_layout(scene.ref(), C.byref(prm), world, 0, C.byref(sky), C.byref(rb),
+                                           C.byref(pb)))
+        rows = lib.rrte_hip_band_rows_for_rank_ex(H, args.band_rows, world, rank, sky.value, rb.value, pb.value)
     primary = W * rows * prm.samples_per_pixel * args.steps
     shadow = int(st.shadow_rays)
 

@@ -416,18 +416,18 @@ uint32_t rrte_hip_band_rows_for_rank(uint32_t height, uint32_t band_rows, int nr
 /* The band partition a multi-GPU frame of `scene` / `params` uses (DESIGN.md §5 "Band partition"): the
  * first *sky_bands bands (bands no object can reach, judged from the camera and the objects' culling
  * spheres: every camera ray there misses) belong to rank 0; the remaining bands go round robin in
- * cycles of L bands.  With k = *root_share in [1, 8] a cycle is one band for rank 0, then k bands for
- * every peer (L = 1 + (nranks - 1) k); with k = 0 rank 0 takes none (L = nranks - 1).  Band b then
- * belongs to: b < sky -> 0; else with q = b - sky, s = q % L: (k && s == 0) -> 0, otherwise
- * 1 + (s - (k ? 1 : 0)) % (nranks - 1).  k is chosen by a work model (sky rows are cheap, the root
- * expands the peers' rows).  Computed identically on every rank; host only.  (env RRTE_BAND_SKY=0:
- * sky 0, root_share 1 -- the plain interleave.)  Rank 0 must be the root for a root-biased partition
- * (otherwise the plain interleave). */
+ * cycles of L = R + (nranks - 1) P bands, R = *root_bands in [0, 8] for rank 0 first, then P =
+ * *peer_bands in [1, 8] rounds of one band per peer.  Band b then belongs to: b < sky -> 0; else with
+ * s = (b - sky) % L: s < R -> 0, otherwise 1 + (s - R) % (nranks - 1).  R:P is chosen by a work model
+ * (sky rows are cheap; the root receives and expands the peers' rows).  Computed identically on every
+ * rank; host only.  (env RRTE_BAND_SKY=0: sky 0, 1:1 -- the plain interleave.)  Rank 0 must be the
+ * root for a root-biased partition (otherwise the plain interleave). */
 rrte_status rrte_hip_band_layout(const rrte_scene_ir* scene, const rrte_render_params* params, int nranks, int root,
-                                 uint32_t* sky_bands, uint32_t* root_share);
-/* Rows owned by `rank` under that partition, in the order they are packed (0 for root_share > 8). */
+                                 uint32_t* sky_bands, uint32_t* root_bands, uint32_t* peer_bands);
+/* Rows owned by `rank` under that partition, in the order they are packed (0 outside the ranges
+ * above, or for root_bands = sky_bands = 0). */
 uint32_t rrte_hip_band_rows_for_rank_ex(uint32_t height, uint32_t band_rows, int nranks, int rank, uint32_t sky_bands,
-                                        uint32_t root_share);
+                                        uint32_t root_bands, uint32_t peer_bands);
 
 #ifdef __cplusplus
 }

@@ -135,8 +135,9 @@ EXPORTS = {
     "rrte_hip_render_gather_async": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_int, _P, _P]),
     "rrte_hip_band_rows_for_rank": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_int, C.c_int]),
     "rrte_hip_band_layout": (C.c_int, [C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_int, C.c_int,
-                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
-    "rrte_hip_band_rows_for_rank_ex": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_uint32, C.c_uint32]),
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "rrte_hip_band_rows_for_rank_ex": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                                    C.c_uint32]),
     "rrte_hip_set_gather_batch": (C.c_int, [_P, C.c_uint32]),
     "rrte_hip_flush": (C.c_int, [_P]),
     "rrte_hip_set_comm_timeout": (C.c_int, [_P, C.c_uint32]),
@@ -176,3 +177,13 @@ class RrteError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"rrte_hip {STATUS_NAMES.get(status, status)}: {msg}")
         self.status = status
+
+
+def band_layout(scene_ref, params_ref, nranks: int, root: int = 0) -> tuple:
+    """(sky_bands, root_bands, peer_bands) of rrte_hip_band_layout (include/rrte_hip.h) for a scene and
+    params passed by reference; raises on an error status."""
+    sky, rb, pb = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    st = load().rrte_hip_band_layout(scene_ref, params_ref, nranks, root, C.byref(sky), C.byref(rb), C.byref(pb))
+    if st != RRTE_OK:
+        raise RuntimeError(f"rrte_hip_band_layout: status {st}")
+    return sky.value, rb.value, pb.value

@@ -90,22 +90,26 @@ __host__ __device__ constexpr uint32_t hot_y(uint32_t h) { return h >> 16; }
 // bands of `band_rows` rows.  The first `sky` bands -- rows no object can reach, judged on the host
 // from the camera and the objects' culling spheres, so every camera ray there misses (the cheapest
 // rows of the frame) -- belong to rank 0 (the root: its rows never cross a link).  The remaining
-// bands go round robin in cycles: with root_share = k >= 1 a cycle is one band for the root, then k
-// bands for every peer (peer order repeated k times); with root_share = 0 the root takes none.
-// sky = 0, root_share = 1 is the plain interleave band % nranks == rank.  A larger k frees the root
+// bands go round robin in cycles of L = root_bands + (nranks - 1) peer_bands bands: first
+// `root_bands` for the root, then `peer_bands` rounds of one band per peer.  sky = 0, root_bands =
+// peer_bands = 1 is the plain interleave band % nranks == rank; a smaller root share frees the root
 // for the expansion of the peers' rows it does per frame.  Which rank renders a band never changes a
 // pixel.
 struct BandMap {
-    uint32_t band_rows, nranks, sky, root_share;
+    uint32_t band_rows, nranks, sky, root_bands, peer_bands;
 };
-__host__ __device__ constexpr uint32_t band_cycle(const BandMap& m) {  // bands per round-robin cycle
-    return (m.root_share ? 1u : 0u) + (m.nranks - 1u) * (m.root_share ? m.root_share : 1u);
+__host__ __device__ constexpr uint32_t band_cycle(const BandMap& m) {
+    return m.root_bands + (m.nranks - 1u) * m.peer_bands;
 }
 // The image band of `rank`'s local band lb.
 __host__ __device__ constexpr uint32_t band_of_local(const BandMap& m, uint32_t rank, uint32_t lb) {
-    const uint32_t L = band_cycle(m), rs = m.root_share ? 1u : 0u, k = m.root_share ? m.root_share : 1u;
-    return rank == 0u ? (lb < m.sky ? lb : m.sky + (lb - m.sky) * L)
-                      : m.sky + (lb / k) * L + rs + (rank - 1u) + (lb % k) * (m.nranks - 1u);
+    const uint32_t L = band_cycle(m);
+    if (rank == 0u) {
+        if (lb < m.sky) return lb;
+        const uint32_t t = lb - m.sky;
+        return m.sky + (t / m.root_bands) * L + t % m.root_bands;
+    }
+    return m.sky + (lb / m.peer_bands) * L + m.root_bands + (rank - 1u) + (lb % m.peer_bands) * (m.nranks - 1u);
 }
 // The rank owning image band b and its local band index there.
 __host__ __device__ constexpr uint32_t band_owner(const BandMap& m, uint32_t b, uint32_t& lb) {
@@ -113,14 +117,13 @@ __host__ __device__ constexpr uint32_t band_owner(const BandMap& m, uint32_t b, 
         lb = b;
         return 0u;
     }
-    const uint32_t L = band_cycle(m), rs = m.root_share ? 1u : 0u, k = m.root_share ? m.root_share : 1u;
-    const uint32_t q = b - m.sky, cyc = q / L, slot = q % L;
-    if (rs && slot == 0u) {
-        lb = m.sky + cyc;
+    const uint32_t L = band_cycle(m), q = b - m.sky, cyc = q / L, slot = q % L;
+    if (slot < m.root_bands) {
+        lb = m.sky + cyc * m.root_bands + slot;
         return 0u;
     }
-    const uint32_t s = slot - rs;
-    lb = cyc * k + s / (m.nranks - 1u);
+    const uint32_t s = slot - m.root_bands;
+    lb = cyc * m.peer_bands + s / (m.nranks - 1u);
     return 1u + s % (m.nranks - 1u);
 }
 
@@ -134,7 +137,7 @@ struct KParams {
     uint32_t rows;           // rows this launch renders
     uint32_t band_rows;      // 0 = identity mapping (+ row0)
     uint32_t nranks, rank;
-    uint32_t sky_bands, root_share;  // band partition (BandMap) of multi-GPU frames
+    uint32_t sky_bands, root_bands, peer_bands;  // band partition (BandMap) of multi-GPU frames
     uint32_t row0;           // first image row of this launch (row-chunked blocking renders; band_rows == 0)
     float bg[4];
     float t_min, bias, inv_gamma, inv_spp;

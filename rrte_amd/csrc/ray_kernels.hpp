@@ -1908,7 +1908,7 @@ __device__ __forceinline__ uint32_t gamma22_u8(float c) {
 __device__ __forceinline__ uint32_t image_row(const KParams& kp, uint32_t r) {
     if (kp.band_rows == 0) return r + kp.row0;
     const uint32_t b = r / kp.band_rows, w = r - b * kp.band_rows;
-    const BandMap m{kp.band_rows, kp.nranks, kp.sky_bands, kp.root_share};
+    const BandMap m{kp.band_rows, kp.nranks, kp.sky_bands, kp.root_bands, kp.peer_bands};
     return band_of_local(m, kp.rank, b) * kp.band_rows + w;
 }
 

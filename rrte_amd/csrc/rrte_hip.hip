@@ -24,6 +24,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <new>
+#include <numeric>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -863,7 +864,8 @@ KParams make_params(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     k.nranks = (uint32_t)c->nranks;
     k.rank = (uint32_t)c->rank;
     k.sky_bands = 0;  // (the plain interleave; plan_launch applies a frame's BandMap)
-    k.root_share = 1;
+    k.root_bands = 1;
+    k.peer_bands = 1;
     memcpy(k.bg, p->background, sizeof k.bg);
     k.t_min = p->t_min;
     k.bias = p->shadow_bias;
@@ -1005,12 +1007,12 @@ void tile_rects(bool enabled, const std::vector<float4>& bounds, const rrte_scen
     k.tile_cull = sh;
 }
 
-constexpr uint32_t kMaxRootShare = 8u;  // largest root_share (peer bands per root band) band_layout picks
+constexpr uint32_t kMaxCycleBands = 8u;  // largest root_bands / peer_bands of a partition
 
 uint32_t rows_for_rank(uint32_t height, uint32_t band_rows, int nranks, int rank, uint32_t sky = 0u,
-                       uint32_t root_share = 1u) {
+                       uint32_t root_bands = 1u, uint32_t peer_bands = 1u) {
     if (nranks <= 1 || band_rows == 0) return height;
-    const BandMap m{band_rows, (uint32_t)nranks, sky, root_share};
+    const BandMap m{band_rows, (uint32_t)nranks, sky, root_bands, peer_bands};
     uint32_t nb = (height + band_rows - 1) / band_rows, rows = 0;
     for (uint32_t b = 0; b < nb; ++b) {
         uint32_t lb = 0;
@@ -1078,31 +1080,42 @@ uint32_t sky_band_count(const rrte_camera& cam, const std::vector<float4>& bound
 
 // The band partition of a multi-GPU frame (BandMap, device_scene.hpp).  The leading "sky" bands --
 // rows above every object's silhouette, where every camera ray misses (the cheapest rows of the
-// frame) -- go to the root; the other bands go round robin, the root taking one band per k of every
-// peer's (root_share = k; 0 = none), k chosen by a work model so the busiest rank is least busy.
+// frame) -- go to the root; the other bands go round robin, root_bands for the root per peer_bands
+// for every peer, the pair chosen by a work model so the busiest rank is least busy.
 // The silhouette top: per object, the cone of directions from the eye that meet its culling sphere,
 // cut at 17 columns across the frame on the image plane (a quadratic per column, double precision),
 // minus one band of margin.  This decides only WHICH rank renders a band -- never a pixel -- so the
 // sampling need not be conservative.  Every rank computes the same partition from the same scene and
-// camera (host arithmetic only).  RRTE_BAND_SKY=0: the plain interleave (sky 0, k 1).
+// camera (host arithmetic only).  RRTE_BAND_SKY=0: the plain interleave (sky 0, 1:1).
 BandMap band_layout(const rrte_camera& cam, const std::vector<float4>& bounds, uint32_t num_prims, uint32_t width,
                     uint32_t height, uint32_t band_rows, int nranks, int root, bool enabled) {
-    BandMap m{band_rows, (uint32_t)std::max(nranks, 1), 0u, 1u};
+    BandMap m{band_rows, (uint32_t)std::max(nranks, 1), 0u, 1u, 1u};
     if (!enabled || nranks <= 1 || root != 0 || band_rows == 0) return m;
     m.sky = sky_band_count(cam, bounds, num_prims, height, band_rows);
-    // The root's round-robin share: the k giving the smallest busiest rank under a work model -- a sky
-    // row costs kSkyCost of an average row (a camera ray that misses: tile profiles put sky tiles at
-    // ~3 us against ~15 us on average), and the root spends kExpandCost of a frame's work expanding
-    // the peers' RGB24 rows (the batched composition, ~3 of ~67 us per 1080p frame)
-    constexpr double kSkyCost = 0.2, kExpandCost = 0.04;
-    const double n = (double)nranks, fs = kSkyCost * m.sky * band_rows / height, rest = 1.0 - fs;
-    double best = std::max(fs + kExpandCost * rest, rest / (n - 1.0));  // k = 0
-    m.root_share = 0u;
-    for (uint32_t k = 1; k <= kMaxRootShare; ++k) {
-        const double L = 1.0 + (n - 1.0) * k;
-        const double load = std::max(fs + rest / L + kExpandCost * rest * (1.0 - 1.0 / L), rest * k / L);
-        if (load < best - 1e-9) best = load, m.root_share = k;
-    }
+    // The root's round-robin share: the (root_bands, peer_bands) pair giving the smallest busiest rank
+    // under a work model over the actual band counts, fitted to emulated rank frames of the 1080p
+    // showcase: a non-sky row costs 1, a sky row kSkyCost (camera rays that miss), and the root spends
+    // kExpandCost per peer row it receives and expands (RCCL receive + the RGB24 expansion); ties
+    // keep the smaller cycle
+    constexpr double kSkyCost = 0.15, kExpandCost = 0.09;
+    const uint32_t nb = (height + band_rows - 1) / band_rows;
+    std::vector<double> load((size_t)nranks);
+    double best = std::numeric_limits<double>::infinity();
+    for (uint32_t a = 0; a <= kMaxCycleBands; ++a)
+        for (uint32_t b = 1; b <= kMaxCycleBands; ++b) {
+            if (a == 0 ? b != 1 : std::gcd(a, b) != 1) continue;  // (one representative per ratio)
+            if (a == 0 && m.sky == 0) continue;                   // (the root would own nothing)
+            const BandMap t{band_rows, (uint32_t)nranks, m.sky, a, b};
+            std::fill(load.begin(), load.end(), 0.0);
+            for (uint32_t band = 0; band < nb; ++band) {
+                uint32_t lb = 0;
+                const uint32_t rows = std::min(band_rows, height - band * band_rows), o = band_owner(t, band, lb);
+                load[o] += band < m.sky ? kSkyCost * rows : (double)rows;
+                if (o != 0) load[0] += kExpandCost * rows;
+            }
+            const double busiest = *std::max_element(load.begin(), load.end());
+            if (busiest < best - 1e-9) best = busiest, m.root_bands = a, m.peer_bands = b;
+        }
     return m;
 }
 
@@ -1244,7 +1257,8 @@ LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_pa
     L.k = make_params(c, s, p, rows);
     if (bm && L.k.band_rows) {
         L.k.sky_bands = bm->sky;
-        L.k.root_share = bm->root_share;
+        L.k.root_bands = bm->root_bands;
+        L.k.peer_bands = bm->peer_bands;
     }
     L.k.row0 = row0;  // (image rows [row0, row0 + rows); band_rows == 0)
     L.k.flags |= internal_flags;
@@ -1283,10 +1297,11 @@ const BandMap& frame_band_map(rrte_ctx* c, const rrte_scene_ir* s, const rrte_re
         bc.root = root;
         bc.rank = c->rank;
         bc.cam = s->camera;
-        bc.rows = rows_for_rank(p->height, p->band_rows, c->nranks, c->rank, bc.m.sky, bc.m.root_share);
+        bc.rows = rows_for_rank(p->height, p->band_rows, c->nranks, c->rank, bc.m.sky, bc.m.root_bands, bc.m.peer_bands);
         bc.cap = 0;
         for (int q = 0; q < c->nranks; ++q)
-            bc.cap = std::max(bc.cap, rows_for_rank(p->height, p->band_rows, c->nranks, q, bc.m.sky, bc.m.root_share));
+            bc.cap = std::max(bc.cap, rows_for_rank(p->height, p->band_rows, c->nranks, q, bc.m.sky, bc.m.root_bands,
+                                                    bc.m.peer_bands));
     }
     if (rows) *rows = bc.rows;
     if (cap) *cap = bc.cap;
@@ -1850,7 +1865,7 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
     const int nr = c->nranks, rk = c->rank;
     uint32_t rows = p->height;
     rrte_render_params pe = *p;
-    BandMap bm{0u, 1u, 0u, 1u};
+    BandMap bm{0u, 1u, 0u, 1u, 1u};
     if (c->emu_nranks > 1) {  // diagnostic: exactly one rank's share of a multi-GPU frame, packed
         c->nranks = c->emu_nranks;
         c->rank = c->emu_rank;
@@ -2021,8 +2036,8 @@ uint32_t rrte_hip_band_rows_for_rank(uint32_t height, uint32_t band_rows, int nr
 }
 
 rrte_status rrte_hip_band_layout(const rrte_scene_ir* s, const rrte_render_params* p, int nranks, int root,
-                                 uint32_t* sky_bands, uint32_t* root_share) {
-    if (!s || !p || !sky_bands || !root_share || nranks < 1 || root < 0 || root >= nranks) return RRTE_INVALID_ARG;
+                                 uint32_t* sky_bands, uint32_t* root_bands, uint32_t* peer_bands) {
+    if (!s || !p || !sky_bands || !root_bands || !peer_bands || nranks < 1 || root < 0 || root >= nranks) return RRTE_INVALID_ARG;
     if ((s->num_prims && !s->prims) || (s->num_mesh_indices && !s->mesh_indices) ||
         (s->num_mesh_vertices && !s->mesh_vertices))
         return RRTE_INVALID_ARG;
@@ -2039,14 +2054,17 @@ rrte_status rrte_hip_band_layout(const rrte_scene_ir* s, const rrte_render_param
     const BandMap m = band_layout(s->camera, bounds, s->num_prims, pp.width, pp.height, pp.band_rows, nranks, root,
                                   !(g && g[0] == '0'));
     *sky_bands = m.sky;
-    *root_share = m.root_share;
+    *root_bands = m.root_bands;
+    *peer_bands = m.peer_bands;
     return RRTE_OK;
 }
 
 uint32_t rrte_hip_band_rows_for_rank_ex(uint32_t height, uint32_t band_rows, int nranks, int rank, uint32_t sky_bands,
-                                        uint32_t root_share) {
-    if (root_share > kMaxRootShare) return 0u;  // (outside the documented range)
-    return rows_for_rank(height, band_rows, nranks, rank, sky_bands, root_share);
+                                        uint32_t root_bands, uint32_t peer_bands) {
+    if (root_bands > kMaxCycleBands || peer_bands < 1u || peer_bands > kMaxCycleBands ||
+        (root_bands == 0u && sky_bands == 0u))
+        return 0u;  // (outside the documented range)
+    return rows_for_rank(height, band_rows, nranks, rank, sky_bands, root_bands, peer_bands);
 }
 
 rrte_status rrte_hip_comm_unique_id(uint8_t out_id[RRTE_UNIQUE_ID_BYTES]) {
@@ -2398,7 +2416,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
     rrte_render_params pp = *p;
     pp.band_rows = band;
     uint32_t rows = p->height, cap = p->height;  // this rank's rows; slab rows (the most any rank owns)
-    const BandMap bm = c->nranks > 1 ? frame_band_map(c, s, &pp, root, &rows, &cap) : BandMap{band, 1u, 0u, 1u};
+    const BandMap bm = c->nranks > 1 ? frame_band_map(c, s, &pp, root, &rows, &cap) : BandMap{band, 1u, 0u, 1u, 1u};
     const bool rgb24 = slab_rgb24(c, s, p);
     // bytes per rank slot, 256-B aligned so every rank's send buffer starts aligned
     const size_t slice = ((size_t)cap * p->width * (rgb24 ? 3u : 4u) + 255u) & ~(size_t)255u;

@@ -145,9 +145,10 @@ extern "C" {
     pub fn rrte_hip_flush(ctx: *mut rrte_ctx) -> rrte_status;
     pub fn rrte_hip_band_rows_for_rank(height: u32, band_rows: u32, nranks: c_int, rank: c_int) -> u32;
     pub fn rrte_hip_band_layout(scene: *const rrte_scene_ir, params: *const rrte_render_params, nranks: c_int,
-                                root: c_int, sky_bands: *mut u32, root_share: *mut u32) -> rrte_status;
+                                root: c_int, sky_bands: *mut u32, root_bands: *mut u32,
+                                peer_bands: *mut u32) -> rrte_status;
     pub fn rrte_hip_band_rows_for_rank_ex(height: u32, band_rows: u32, nranks: c_int, rank: c_int, sky_bands: u32,
-                                          root_share: u32) -> u32;
+                                          root_bands: u32, peer_bands: u32) -> u32;
 }
 
 pub mod safe;

@@ -100,34 +100,37 @@ def test_fpcheck_rejects_bad_ranges():
     assert lib.rrte_hip_fpcheck(0, abi.FPCHECK_SQRT, 0, 1, None) == 1
 
 
-def _band_of_local(rank, lb, n, sky, rs):
-    """Mirror of device_scene.hpp band_of_local (rs = root_share k: one root band per k of every peer's)."""
-    L = 1 + (n - 1) * rs if rs else n - 1
+def _band_of_local(rank, lb, n, sky, rb, pb):
+    """Mirror of device_scene.hpp band_of_local (rb root bands, then pb rounds over the peers, per cycle)."""
+    L = rb + (n - 1) * pb
     if rank == 0:
-        return lb if lb < sky else sky + (lb - sky) * L
-    k = rs or 1
-    return sky + (lb // k) * L + (1 if rs else 0) + (rank - 1) + (lb % k) * (n - 1)
+        if lb < sky:
+            return lb
+        t = lb - sky
+        return sky + (t // rb) * L + t % rb
+    return sky + (lb // pb) * L + rb + (rank - 1) + (lb % pb) * (n - 1)
 
 
 @pytest.mark.parametrize("H,band,n", [(1080, 16, 2), (1080, 16, 8), (2160, 16, 8), (1000, 16, 3), (7, 16, 4),
                                       (480, 16, 8), (1080, 8, 5)])
-@pytest.mark.parametrize("sky,rs", [(0, 1), (3, 1), (16, 0), (16, 1), (40, 0), (0, 2), (12, 3), (5, 8)])
-def test_sky_band_partition_covers_every_row_once(H, band, n, sky, rs):
+@pytest.mark.parametrize("sky,rb,pb", [(0, 1, 1), (3, 1, 1), (16, 0, 1), (16, 1, 1), (40, 0, 1), (0, 1, 2), (12, 1, 3),
+                                       (5, 1, 8), (0, 2, 3), (7, 3, 4), (9, 8, 1)])
+def test_sky_band_partition_covers_every_row_once(H, band, n, sky, rb, pb):
     """rrte_hip_band_rows_for_rank_ex and the device mapping (band_of_local) for a partition with sky
     bands on rank 0: every image row exactly once, packed in image order per rank."""
     lib = abi.load()
     nb = (H + band - 1) // band
     sky = min(sky, nb - 1)
-    if rs == 0 and sky == 0:
+    if rb == 0 and sky == 0:
         return  # (not a layout band_layout produces: the root would own nothing)
-    rows = [lib.rrte_hip_band_rows_for_rank_ex(H, band, n, r, sky, rs) for r in range(n)]
+    rows = [lib.rrte_hip_band_rows_for_rank_ex(H, band, n, r, sky, rb, pb) for r in range(n)]
     assert sum(rows) == H
     seen = []
     for r in range(n):
         prev = -1
         for lr in range(rows[r]):
             b, w = divmod(lr, band)
-            y = _band_of_local(r, b, n, sky, rs) * band + w
+            y = _band_of_local(r, b, n, sky, rb, pb) * band + w
             assert y > prev  # packed in image order
             prev = y
             seen.append(y)
@@ -142,16 +145,19 @@ def test_band_layout_of_the_showcase():
     objs, lights, cam, cfg = scenes.sdf_showcase(1920, 1080)
     cfg.band_rows = 16
     sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
-    sky, rs = C.c_uint32(), C.c_uint32()
+    sky, rb, pb = C.c_uint32(), C.c_uint32(), C.c_uint32()
 
-    def layout(n):
-        assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), n, 0, C.byref(sky), C.byref(rs)) == abi.RRTE_OK
-        return sky.value, rs.value
-    s8, rs8 = layout(8)
-    assert 8 <= s8 < 34 and 2 <= rs8 <= 8  # ~a quarter of the rows is sky; at 8 ranks a small root share
-    assert layout(2)[1] == 1  # at 2 ranks the root also takes a round-robin share
-    assert layout(1) == (0, 1)
-    assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), 8, 3, C.byref(sky), C.byref(rs)) == abi.RRTE_OK
-    assert (sky.value, rs.value) == (0, 1)  # a root other than rank 0: the plain interleave
-    assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), 0, 0, C.byref(sky), C.byref(rs)) == abi.RRTE_INVALID_ARG
-    assert lib.rrte_hip_band_rows_for_rank_ex(1080, 16, 8, 1, 0, 9) == 0  # root_share beyond 8: rejected
+    def layout(n, root=0):
+        assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), n, root, C.byref(sky), C.byref(rb),
+                                        C.byref(pb)) == abi.RRTE_OK
+        return sky.value, rb.value, pb.value
+    s8, rb8, pb8 = layout(8)
+    assert 8 <= s8 < 34 and rb8 < pb8  # ~a quarter of the rows is sky; at 8 ranks a smaller root share
+    s2, rb2, pb2 = layout(2)
+    assert s2 == s8 and rb2 >= 1  # at 2 ranks the root also takes a round-robin share
+    assert layout(1) == (0, 1, 1)
+    assert layout(8, root=3) == (0, 1, 1)  # a root other than rank 0: the plain interleave
+    assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), 0, 0, C.byref(sky), C.byref(rb),
+                                    C.byref(pb)) == abi.RRTE_INVALID_ARG
+    for bad in [(0, 9, 1), (0, 1, 0), (0, 1, 9), (0, 0, 1)]:  # outside the documented ranges
+        assert lib.rrte_hip_band_rows_for_rank_ex(1080, 16, 8, 1, *bad) == 0

@@ -51,16 +51,12 @@ def test_sdf_showcase_4k_matches_oracle(jit):
     compare(*scenes.sdf_showcase(W, H), threads=16, jit=jit)
 
 
-def band_owner(b, n, sky, root_share):
+def band_owner(b, n, sky, rb, pb):
     """The rank owning image band b (include/rrte_hip.h rrte_hip_band_layout)."""
     if b < sky or n == 1:
         return 0
-    k = root_share
-    L = (1 + (n - 1) * k) if k else n - 1
-    s = (b - sky) % L
-    if k and s == 0:
-        return 0
-    return 1 + (s - (1 if k else 0)) % (n - 1)
+    s = (b - sky) % (rb + (n - 1) * pb)
+    return 0 if s < rb else 1 + (s - rb) % (n - 1)
 
 
 @pytest.mark.parametrize("sky_on", ["1", "0"])
@@ -77,16 +73,14 @@ def test_4k_rank_shares_match_oracle_rows(nranks, sky_on, oracle_4k, monkeypatch
     prm.flags |= abi.FLAG_F32_LINEAR
     lib = abi.load()
     monkeypatch.setenv("RRTE_BAND_SKY", sky_on)
-    sky, rs = C.c_uint32(), C.c_uint32()
-    assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), nranks, 0, C.byref(sky), C.byref(rs)) == abi.RRTE_OK
-    sky, rs = sky.value, rs.value
+    sky, rb, pb = abi.band_layout(sc.ref(), C.byref(prm), nranks)
     assert (sky > 0) == (sky_on == "1")  # the 4K showcase has sky rows above every object
     total = 0
     for rank in range(nranks):
         monkeypatch.setenv("RRTE_EMULATE_RANK", f"{nranks}:{rank}")
         ctx = Context(0, jit=abi.JIT_ON)
-        rows = lib.rrte_hip_band_rows_for_rank_ex(H, BAND, nranks, rank, sky, rs)
-        img_rows = [y for y in range(H) if band_owner(y // BAND, nranks, sky, rs) == rank]
+        rows = lib.rrte_hip_band_rows_for_rank_ex(H, BAND, nranks, rank, sky, rb, pb)
+        img_rows = [y for y in range(H) if band_owner(y // BAND, nranks, sky, rb, pb) == rank]
         assert len(img_rows) == rows
         f32 = torch.zeros(rows * W * 4, dtype=torch.float32, device="cuda")
         torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
@@ -98,7 +92,7 @@ def test_4k_rank_shares_match_oracle_rows(nranks, sky_on, oracle_4k, monkeypatch
         bad = (got != want).any(-1)
         assert not bad.any(), f"rank {rank}/{nranks}: {int(bad.sum())} pixels differ from the oracle"
         assert st.jit_active == 1
-        assert int(st.shadow_rays) == sum(band_shadow[b] for b in range(NBANDS) if band_owner(b, nranks, sky, rs) == rank), rank
+        assert int(st.shadow_rays) == sum(band_shadow[b] for b in range(NBANDS) if band_owner(b, nranks, sky, rb, pb) == rank), rank
         total += int(st.shadow_rays)
         ctx.close()
     assert total == sum(band_shadow)

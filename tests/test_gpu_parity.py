@@ -324,10 +324,9 @@ def test_camera_tile_culling_with_band_mapping(band, jit, monkeypatch):
             prm = cfg.lower()
             prm.flags |= abi.FLAG_F32_LINEAR
             # this pose's band partition (sky bands on rank 0, the rest round robin)
-            sky, rs = C.c_uint32(), C.c_uint32()
-            assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), nranks, 0, C.byref(sky), C.byref(rs)) == 0
-            rows = lib.rrte_hip_band_rows_for_rank_ex(h, band, nranks, rank, sky.value, rs.value)
-            img_rows = [y for y in range(h) if band_owner(y // band, nranks, sky.value, rs.value) == rank]
+            part = abi.band_layout(sc.ref(), C.byref(prm), nranks)
+            rows = lib.rrte_hip_band_rows_for_rank_ex(h, band, nranks, rank, *part)
+            img_rows = [y for y in range(h) if band_owner(y // band, nranks, *part) == rank]
             assert len(img_rows) == rows
             out = {}
             for tc, ctx in ctxs.items():

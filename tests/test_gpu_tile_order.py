@@ -93,9 +93,7 @@ def test_fixed_tile_list_on_band_mapped_ranks(nranks, rank, monkeypatch):
     cfg.band_rows = band
     sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
     lib = abi.load()
-    sky, rs = C.c_uint32(), C.c_uint32()
-    assert lib.rrte_hip_band_layout(sc.ref(), C.byref(prm), nranks, 0, C.byref(sky), C.byref(rs)) == abi.RRTE_OK
-    rows = lib.rrte_hip_band_rows_for_rank_ex(h, band, nranks, rank, sky.value, rs.value)
+    rows = lib.rrte_hip_band_rows_for_rank_ex(h, band, nranks, rank, *abi.band_layout(sc.ref(), C.byref(prm), nranks))
     env = {"RRTE_EMULATE_RANK": f"{nranks}:{rank}"}
     ref = _ctx(monkeypatch, "0", abi.JIT_ON, **env)
     hot = _ctx(monkeypatch, "2", abi.JIT_ON, **env)
