@@ -206,6 +206,19 @@ __device__ __forceinline__ bool mask_lane(uint64_t m) { return mask_select(m, 0.
 // (breaks parity), never a build setting.
 #ifdef RRTE_ABLATE_FAST_SQRT
 __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_amdgcn_sqrtf(x); }
+#elif defined(RRTE_SQRT_BRANCHFREE)
+__device__ __forceinline__ float sqrt_rn(float x) {
+    // the same residual correction with no branch: x below 2^-96 is scaled by 2^64 first and the
+    // root by 2^-32 after (both exact); +-0 and +inf, where rsq gives inf / 0 and s = x * y is NaN,
+    // return x through one v_cmp_class; negatives and NaNs come out NaN from rsq
+    const bool tiny = x < 0x1p-96f;
+    const float xs = x * (tiny ? 0x1p+64f : 1.0f);
+    const float y = __builtin_amdgcn_rsqf(xs);
+    const float s = xs * y;
+    const float e = __builtin_fmaf(-s, s, xs);
+    const float r = __builtin_fmaf(e, 0.5f * y, s) * (tiny ? 0x1p-32f : 1.0f);
+    return __builtin_amdgcn_classf(xs, 0x060 | 0x200) ? xs : r;  // +-0 (0x20, 0x40), +inf (0x200)
+}
 #else
 __device__ __forceinline__ float sqrt_rn(float x) {
     // one residual correction from a single transcendental: y = v_rsq_f32(x), s = x * y (faithful),

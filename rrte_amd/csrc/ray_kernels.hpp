@@ -569,7 +569,7 @@ __device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float
 #ifndef RRTE_MARCH_UNROLL
 #define RRTE_MARCH_UNROLL 1
 #endif
-// RRTE_MARCH_PRED (A/B switch, bit-exact at every level; tools/r03_ab.sh): 0 divergent-exit march loops
+// RRTE_MARCH_PRED (A/B switch, bit-exact at every level; tools/jit_ab.sh): 0 divergent-exit march loops
 // (default); 1 the predicated loop (sdf_march_loop) after the divergent bound test; 2 + a predicated
 // bound test (the loop runs under the caller's EXEC); 3 + predicated shadow rays (every lane of the
 // wave runs every any-hit test).  Measured on the headline (two interleaved rounds each): 1 = lone

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of scene-specialised kernel build options (RRTE_JIT_EXTRA_OPTS), interleaved rounds: headline
 # (200 and 20 steps) and the 4K deformation stress.  Then the parity subset under the LAST variant.
-# usage: bash tools/r03_ab.sh "<opts A>" "<opts B>" ...   ("" = defaults)
+# usage: bash tools/jit_ab.sh "<opts A>" "<opts B>" ...   ("" = defaults)
 set -o pipefail
 mkdir -p gpurun_out
 OUT=gpurun_out/r03_ab.txt

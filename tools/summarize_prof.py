@@ -1,4 +1,4 @@
-"""Summarize a tools/prof_gpu.sh output dir into profiles/<name>.md and profiles/pmc_<name>.json.
+"""Summarize a tools/prof.sh output dir into profiles/<name>.md and profiles/pmc_<name>.json.
 
 usage: python tools/summarize_prof.py gpurun_out/prof_<tag> <name> <workload-key>
 <workload-key> must be bench.py's key (e.g. sdf-showcase@1920x1080/lambert_shadow): bench.py takes the
