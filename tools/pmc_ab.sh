@@ -5,7 +5,8 @@
 #   e.g. tools/pmc_ab.sh 2 "base|" "noguard|RRTE_JIT_EXTRA_OPTS=-DRRTE_ABLATE_NO_GUARDS" "primary|RRTE_DEBUG=2"
 # Device-code variants go through RRTE_JIT_EXTRA_OPTS (the scene-specialised kernel is compiled at run
 # time; the disk-cache key includes the options).  Output: gpurun_out/pmc_ab/<name>_r<k>/ and a table
-# on stdout.  Every step has its own time limit; the first failure ends the run.
+# on stdout.  Every step has its own time limit; the first failure ends the run.  PMC_COUNTERS replaces
+# the counter set (one pass; e.g. "FETCH_SIZE" or "WRITE_SIZE" -- the block limits of rocprofv3 apply).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 ROUNDS=${1:?rounds}; shift
@@ -13,7 +14,7 @@ OUT=$R/gpurun_out/pmc_ab
 mkdir -p $OUT
 export GPU_MAX_HW_QUEUES=32  # (under rocprofv3 HIP starts before bench.py could set it)
 cd /tmp && export TMPDIR=/tmp
-COUNTERS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+COUNTERS=${PMC_COUNTERS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES"}
 for k in $(seq 1 $ROUNDS); do
   for spec in "$@"; do
     name=${spec%%|*}; envs=${spec#*|}
@@ -44,10 +45,12 @@ c = {n: sum(v) / len(v) for n, v in acc.items()}
 res = {"name": name, "round": int(k), "ms200": m200, "ms20": m20, "launch_ms": lone, "u8_max_diff": vd,
        "VALU_M": c.get("SQ_INSTS_VALU", 0) / 1e6, "SALU_M": c.get("SQ_INSTS_SALU", 0) / 1e6,
        "SMEM_M": c.get("SQ_INSTS_SMEM", 0) / 1e6, "VMEM_RD_M": c.get("SQ_INSTS_VMEM_RD", 0) / 1e6,
-       "waves": c.get("SQ_WAVES", 0), "dispatches": len(acc.get("SQ_INSTS_VALU", []))}
+       "waves": c.get("SQ_WAVES", 0), "dispatches": max((len(v) for v in acc.values()), default=0),
+       "counters": c}
 json.dump(res, open(d / "summary.json", "w"))
 print(f"{name:>14} r{k}  200st {m200:.4f}  20st {m20:.4f}  launch {lone:.4f}  VALU {res['VALU_M']:.2f}M  "
-      f"SALU {res['SALU_M']:.2f}M  SMEM {res['SMEM_M']:.2f}M  VMEM_RD {res['VMEM_RD_M']:.3f}M  u8diff {vd}", flush=True)
+      f"SALU {res['SALU_M']:.2f}M  SMEM {res['SMEM_M']:.2f}M  VMEM_RD {res['VMEM_RD_M']:.3f}M  u8diff {vd}"
+      + "".join(f"  {n} {v:.1f}" for n, v in c.items() if not n.startswith("SQ_")), flush=True)
 PY
   done
 done
