@@ -279,6 +279,7 @@ struct rrte_ctx {
     hipEvent_t ev_bcopy = nullptr;
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed scrambled permutation of the tiles (tests)
+    bool env_tile_xcd = false;          // RRTE_TILE_XCD=1: XCD-aware LPT (lpt_slots_xcd; A/B experiment)
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
     // per launch, so the version pool wraps within a few frames)
     bool env_test_recycle = false;
@@ -1341,6 +1342,33 @@ std::vector<uint32_t> lpt_slots(const uint32_t* costs, uint32_t n, uint32_t tile
     return slots;
 }
 
+// XCD-aware LPT (RRTE_TILE_XCD=1, A/B experiment): the four tiles of a tile row that share each 128-B
+// line of the frame (32 RGBA8 pixels) take slots k, k+8, k+16, k+24 -- workgroups b and b+8 share an
+// XCD under round-robin dispatch (MI355X_MICROARCH.md; for speed only, never for correctness) and
+// start together -- with the groups in LPT order of their slowest tile.  Every tile once.
+std::vector<uint32_t> lpt_slots_xcd(const uint32_t* costs, uint32_t n, uint32_t tiles_x) {
+    std::vector<uint32_t> slots;
+    if (n == 0 || tiles_x == 0) return slots;
+    const uint32_t gx = (tiles_x + 3u) / 4u, rows = n / tiles_x, ng = gx * rows;
+    std::vector<uint32_t> gcost(ng, 0u), order(ng);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t& g = gcost[(i / tiles_x) * gx + (i % tiles_x) / 4u];
+        g = std::max(g, costs[i]);
+    }
+    for (uint32_t g = 0; g < ng; ++g) order[g] = g;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return gcost[a] > gcost[b]; });
+    slots.reserve(n);
+    for (uint32_t base = 0; base < ng; base += 8u) {
+        const uint32_t m = std::min(8u, ng - base);
+        for (uint32_t i = 0; i < 4u; ++i)
+            for (uint32_t j = 0; j < m; ++j) {
+                const uint32_t g = order[base + j], x = (g % gx) * 4u + i;
+                if (x < tiles_x) slots.push_back(hot_pack(x, g / gx));
+            }
+    }
+    return slots;
+}
+
 // RRTE_TILE_ORDER=2 (tests): every tile once in a fixed scrambled order -- slot k takes tile
 // (k * stride) mod n for a stride near 0.618 n coprime with n -- so the list path runs on every launch
 // without a profile.
@@ -1435,8 +1463,10 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
             // counting sort takes ~0.5 ms of host time that a render call must not stall for
             std::vector<uint32_t> costs(tp.h_cost, tp.h_cost + tp.tiles);
             const uint32_t tx = tp.tiles_x;
-            tp.work = std::async(std::launch::async, [key, costs = std::move(costs), tx]() {
-                return TilePlanResult{key, lpt_slots(costs.data(), (uint32_t)costs.size(), tx)};
+            const bool xcd = c->env_tile_xcd;
+            tp.work = std::async(std::launch::async, [key, costs = std::move(costs), tx, xcd]() {
+                return TilePlanResult{key, xcd ? lpt_slots_xcd(costs.data(), (uint32_t)costs.size(), tx)
+                                               : lpt_slots(costs.data(), (uint32_t)costs.size(), tx)};
             });
             tp.working = true;
             tp.launches = 0;
@@ -1725,6 +1755,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_BAND_SKY")) c->env_band_sky = g[0] != '0';
     if (const char* g = getenv("RRTE_COMM_PRIORITY")) c->env_comm_priority = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
+    if (const char* g = getenv("RRTE_TILE_XCD")) c->env_tile_xcd = g[0] == '1';
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
         c->env_tile_order_fixed = g[0] == '2';  // 0 image order, 2 fixed permutation (tests), else measured (default)
