@@ -153,6 +153,10 @@ struct KParams {
     uint32_t* tile_cost;     // non-null: frame 0's workgroups store their duration (100 MHz ticks) at [y * tiles_x + x]
     const uint32_t* hot;     // device tile list (hot_n words; immutable while launches use it)
     uint32_t tiles_x, hot_n;
+    // slots [0, prio_slots) of the list -- the slowest tiles -- raise their wave's issue priority
+    // (s_setprio): on a SIMD shared with cheap waves the frame's critical chains issue first (A/B
+    // switch RRTE_PRIO_SLOTS; 0 = off)
+    uint32_t prio_slots;
     // Output rows: 0 = this launch's rows packed (row r at r * width, frame z at out + z * frame_stride),
     // 1 = at their image rows of frame z's own buffer cam[z].out (image_row(r) * width: a multi-GPU
     // root renders its own bands straight into the final frames; RGBA8 only)

@@ -1954,6 +1954,7 @@ __device__ __forceinline__ LaunchTile launch_tile(const KParams& kp) {
         const uint32_t h = kp.hot[t.run ? k : 0u];
         t.x = hot_x(h);
         t.y = hot_y(h);
+        if (k < kp.prio_slots) __builtin_amdgcn_s_setprio(2);
     }
     return t;
 }

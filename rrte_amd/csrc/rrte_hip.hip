@@ -280,6 +280,7 @@ struct rrte_ctx {
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed scrambled permutation of the tiles (tests)
     bool env_tile_xcd = false;          // RRTE_TILE_XCD=1: XCD-aware LPT (lpt_slots_xcd; A/B experiment)
+    uint32_t env_prio_slots = 0;        // RRTE_PRIO_SLOTS=N: the list's first N slots raise wave priority (A/B)
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
     // per launch, so the version pool wraps within a few frames)
     bool env_test_recycle = false;
@@ -1446,6 +1447,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     k.tiles_x = L.gx;
     k.hot = nullptr;
     k.hot_n = 0;
+    k.prio_slots = 0;
     k.tile_cost = nullptr;
     // (RRTE_DEBUG bit 5 runs one workgroup in image-order numbering: no tile order; bit 4's per-wave
     // stamps work with it)
@@ -1509,6 +1511,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     if (!tp.slots.empty() && tp.slots.size() == tiles && (tp.cur >= 0 || upload_hot_list(c, tp))) {
         k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
+        k.prio_slots = std::min(c->env_prio_slots, k.hot_n);
         tp.ret[tp.cur].use(st);
     }
     if (!profile) return false;
@@ -1756,6 +1759,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_COMM_PRIORITY")) c->env_comm_priority = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_TILE_XCD")) c->env_tile_xcd = g[0] == '1';
+    if (const char* g = getenv("RRTE_PRIO_SLOTS")) c->env_prio_slots = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
         c->env_tile_order_fixed = g[0] == '2';  // 0 image order, 2 fixed permutation (tests), else measured (default)
