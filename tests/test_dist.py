@@ -1,4 +1,4 @@
-"""Multi-rank row-band composition on CPU (gloo, world_size 2 and 3), in the layout of the batched GPU
+"""Multi-rank row-band composition on CPU (gloo, world_size 2, 3 and 4), in the layout of the batched GPU
 path (rrte_hip.hip render_batch / flush_batch): each rank renders the bands the frame's band partition
 gives it (rrte_hip_band_layout: sky bands on the root, the rest round robin at the root:peer ratio;
 the oracle stands in for the per-rank kernel); the ROOT writes its own bands straight into the frame at their
@@ -89,7 +89,7 @@ def _worker(rank, n, port, scene_name, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 4])
 def test_band_gather_composition_matches_single_frame(n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
