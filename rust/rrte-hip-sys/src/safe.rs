@@ -165,6 +165,36 @@ impl Context {
     }
 }
 
+/// The band partition of a multi-GPU frame (include/rrte_hip.h rrte_hip_band_layout): the number of
+/// leading bands rank 0 renders because no object reaches them, then the round-robin ratio -- root
+/// bands, then peer bands per peer, per cycle.  Host arithmetic only; every rank gets the same answer.
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub struct BandLayout {
+    pub sky_bands: u32,
+    pub root_bands: u32,
+    pub peer_bands: u32,
+}
+
+impl BandLayout {
+    pub fn of(scene: &SceneIr, params: &rrte_render_params, nranks: i32, root: i32) -> Result<BandLayout, Error> {
+        let ir = scene.raw();
+        let (mut sky, mut rb, mut pb) = (0u32, 0u32, 0u32);
+        let st = unsafe { rrte_hip_band_layout(&ir, params, nranks, root, &mut sky, &mut rb, &mut pb) };
+        if st != RRTE_OK {
+            return Err(Error { status: st, message: "rrte_hip_band_layout failed".into() });
+        }
+        Ok(BandLayout { sky_bands: sky, root_bands: rb, peer_bands: pb })
+    }
+
+    /// Rows `rank` renders under this partition (packed in image order).
+    pub fn rows_for_rank(&self, height: u32, band_rows: u32, nranks: i32, rank: i32) -> u32 {
+        unsafe {
+            rrte_hip_band_rows_for_rank_ex(height, band_rows, nranks, rank, self.sky_bands, self.root_bands,
+                                           self.peer_bands)
+        }
+    }
+}
+
 impl Drop for Context {
     fn drop(&mut self) {
         unsafe { rrte_hip_destroy(self.ctx) };

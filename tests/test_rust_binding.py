@@ -242,6 +242,35 @@ def test_python_bindings_cover_the_header():
     assert set(abi.EXPORTS) == set(header_functions())
 
 
+def _rust_ffi_calls(text):
+    """(name, argument count) of every `rrte_hip_*(...)` call in Rust source (parentheses balanced)."""
+    out = []
+    for m in re.finditer(r"\b(rrte_hip_\w+)\(", text):
+        depth, i = 1, m.end()
+        while depth and i < len(text):
+            depth += {"(": 1, ")": -1}.get(text[i], 0)
+            i += 1
+        inner = text[m.end():i - 1].strip()
+        out.append((m.group(1), 0 if not inner else len(_split_top(inner))))
+    return out
+
+
+def test_safe_wrappers_call_the_ffi_with_the_declared_arity():
+    """Every FFI call in the safe wrapper and the backend crate passes as many arguments as the header
+    declares (no cargo here: a wrapper left behind by a signature change would not be compiled)."""
+    hf = header_functions()
+    files = [ROOT / "rust" / "rrte-hip-sys" / "src" / "safe.rs", ROOT / "rust" / "rrte-renderer-hip" / "src" / "lib.rs"]
+    calls = []
+    for f in files:
+        t = _strip_comments(f.read_text())
+        t = re.sub(r"pub fn rrte_hip_\w+\(", "pub fn X(", t)  # (declarations are checked above)
+        calls += _rust_ffi_calls(t)
+    assert len(calls) >= 10
+    for name, n in calls:
+        assert name in hf, name
+        assert n == len(hf[name][1]), f"{name}: {n} arguments, header declares {len(hf[name][1])}"
+
+
 @pytest.mark.parametrize("mutate", ["swap", "width"])
 def test_checker_catches_a_layout_drift(mutate, tmp_path):
     """The checker itself: a swapped field or a wrong field type must be caught."""
