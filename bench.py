@@ -3,8 +3,8 @@
 python bench.py --gpus N --steps K --warmup W
   N = 1: one rrte_hip_render_async frame per step on cuda:0.
   N > 1: launched by torch.distributed.run; every rank renders its interleaved
-         16-row bands of the SAME 1080p frame and the frame is gathered to rank 0
-         over RCCL/xGMI (rrte_hip_render_gather_async) -> strong scaling.
+         16-row bands of the SAME 1080p frame (the frame's band partition) and the frame
+         is composed on rank 0 over RCCL/xGMI send/recv (rrte_hip_render_gather_async) -> strong scaling.
 A "step" is one frame.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -287,14 +287,12 @@ def main():
         cfg.jitter = "random"
     scene = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
-    # N > 1: frames are gathered in batches of F (rrte_hip_set_gather_batch): each batch renders in
-    # multi-frame launches (8 frames per launch) on the library's render streams and ONE ncclGather
-    # per batch on its comm stream moves it to rank 0.  Per-frame gathers chained across streams cost
-    # 50-90 us per rank-sized 1920x136 frame against 15 us for its render; batches of 8 / 16 cost
-    # 14 / 12 us per frame, gather and de-interleave included (tools/gather_variants.py, one GPU
-    # through a 1-rank communicator, 400 frames); at the driver's 20 steps batches of 8 keep the
-    # last batch's gather (link-bound at N > 1) short.  Every frame is still gathered to rank 0 and
-    # de-interleaved inside the timed region (flushed before its end).
+    # N > 1: frames are exchanged in batches of F (rrte_hip_set_gather_batch): each batch renders in
+    # multi-frame launches (8 frames per launch) on the library's render streams -- rank 0 writing its
+    # own bands straight into the frame buffers -- and ONE grouped ncclSend / ncclRecv per batch on its
+    # comm stream moves the peers' RGB24 rows to rank 0, which expands them.  Batches of
+    # 8 keep the last batch's exchange short at the driver's 20 steps.  Every frame is still composed
+    # on rank 0 inside the timed region (the last batch is flushed before its end).
     ctx = Context(local_rank, jit={"off": abi.JIT_OFF, "on": abi.JIT_ON, "auto": abi.JIT_AUTO}[args.jit])
     lib = ctx.lib
 
@@ -514,7 +512,7 @@ def main():
             "config": {
                 "workload": f"{args.scene} {W}x{H}, {args.mode}, spp={prm.samples_per_pixel}, max_depth={prm.max_depth}, "
                             + ("random jitter" if args.random else "pixel-centre jitter")
-                            + (f", {args.band_rows}-row bands interleaved over {world} GPUs + RCCL gather to rank 0"
+                            + (f", {args.band_rows}-row bands over {world} GPUs (sky bands on rank 0, the rest round robin) + RCCL send/recv to rank 0"
                                f" in batches of {min(F, 16)} frames" if world > 1 else "")
                             + (", REHEARSAL: gather path through a 1-rank communicator" if gath and not dist_on else ""),
                 "scene": args.scene, "width": W, "height": H, "mode": args.mode,
