@@ -334,10 +334,12 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* scene, int mode, char* log, 
 /*   RRTE_FPCHECK_SQRT_HW: control -- the bare v_sqrt_f32 against the correctly rounded sqrt
  *                         (the sweep must find its 1-ulp errors).
  *   RRTE_FPCHECK_GAMMA_U8: every f32 bit pattern in [lo, hi): the kernels' gamma-2.2 byte
- *                          (ray_kernels.hpp gamma22_u8) against to_u8(clamp(powf(c, 1/2.2))). */
+ *                          (ray_kernels.hpp gamma22_u8) against to_u8(clamp(powf(c, 1/2.2))).
+ *   RRTE_FPCHECK_SQRT_BF: as RRTE_FPCHECK_SQRT for the branch-free form (sqrt_rn_branchfree);
+ *                         RRTE_FPCHECK_SQRT sweeps the guarded form (sqrt_rn_guarded). */
 typedef enum rrte_fpcheck {
     RRTE_FPCHECK_SQRT = 0, RRTE_FPCHECK_RCP = 1, RRTE_FPCHECK_DIV = 2, RRTE_FPCHECK_SQRT_HW = 3,
-    RRTE_FPCHECK_GAMMA_U8 = 4
+    RRTE_FPCHECK_GAMMA_U8 = 4, RRTE_FPCHECK_SQRT_BF = 5
 } rrte_fpcheck;
 rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uint64_t* mismatches);
 /* Diagnostic (host only): the CSG early-out decoration the renderer applies to one SDF program
@@ -409,6 +411,11 @@ rrte_status rrte_hip_set_comm_timeout(rrte_ctx* ctx, uint32_t ms);
  * same setting.  Flushing with no open batch does nothing. */
 rrte_status rrte_hip_set_gather_batch(rrte_ctx* ctx, uint32_t frames);
 rrte_status rrte_hip_flush(rrte_ctx* ctx);
+/* Diagnostic: the collectives this context has issued on its communicator since rrte_hip_comm_init
+ * (per-frame gathers and batch exchanges) and the frames of the open gather batch.  A local call
+ * (rrte_hip_synchronize, a scene change) renders the open batch but never issues a collective, so
+ * neither count may move on one rank alone. */
+rrte_status rrte_hip_gather_info(rrte_ctx* ctx, uint64_t* collectives, uint32_t* open_frames);
 
 /* Host-side helpers exported for the bindings (no device work). */
 /* Rows owned by `rank` under the plain band interleave (band b on rank b % nranks). */

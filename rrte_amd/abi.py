@@ -35,7 +35,7 @@ SDF_POP_POINT = 96
 SDF_MAX_STACK, SDF_MAX_POINT_STACK, SDF_MAX_OCTAVES = 8, 4, 8
 UNIQUE_ID_BYTES = 128
 JIT_OFF, JIT_ON, JIT_AUTO = 0, 1, 2
-FPCHECK_SQRT, FPCHECK_RCP, FPCHECK_DIV, FPCHECK_SQRT_HW, FPCHECK_GAMMA_U8 = 0, 1, 2, 3, 4
+FPCHECK_SQRT, FPCHECK_RCP, FPCHECK_DIV, FPCHECK_SQRT_HW, FPCHECK_GAMMA_U8, FPCHECK_SQRT_BF = 0, 1, 2, 3, 4, 5
 
 
 # --------------------------------------------------------------- structs
@@ -140,6 +140,7 @@ EXPORTS = {
                                                     C.c_uint32]),
     "rrte_hip_set_gather_batch": (C.c_int, [_P, C.c_uint32]),
     "rrte_hip_flush": (C.c_int, [_P]),
+    "rrte_hip_gather_info": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "rrte_hip_set_comm_timeout": (C.c_int, [_P, C.c_uint32]),
 }
 

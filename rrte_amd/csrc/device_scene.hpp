@@ -208,13 +208,12 @@ __device__ __forceinline__ bool mask_lane(uint64_t m) { return mask_select(m, 0.
 // x - s*(s -/+ ulp) changes sign, guarded below 2^-96 -- took 11.)
 // RRTE_ABLATE_FAST_SQRT swaps in the bare 1-ulp v_sqrt_f32 -- a timing experiment only
 // (breaks parity), never a build setting.
-#ifdef RRTE_ABLATE_FAST_SQRT
-__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_amdgcn_sqrtf(x); }
-#elif defined(RRTE_SQRT_BRANCHFREE)
-__device__ __forceinline__ float sqrt_rn(float x) {
-    // the same residual correction with no branch: x below 2^-96 is scaled by 2^64 first and the
-    // root by 2^-32 after (both exact); +-0 and +inf, where rsq gives inf / 0 and s = x * y is NaN,
-    // return x through one v_cmp_class; negatives and NaNs come out NaN from rsq
+// Branch-free form of the same residual correction (RRTE_FPCHECK_SQRT_BF sweeps it over all 2^32
+// inputs): x below 2^-96 is scaled by 2^64 first and the root by 2^-32 after (both exact: the scaled
+// x is a normal in [2^-85, 2^-32), its root a normal); +-0 and +inf, where rsq gives inf / 0 and
+// s = x * y is NaN, return x through one v_cmp_class; negatives and NaNs come out NaN from rsq.  No
+// EXEC save / restore, so neighbouring roots share basic blocks (and v_pk_mul / v_pk_fma pairs).
+__device__ __forceinline__ float sqrt_rn_branchfree(float x) {
     const bool tiny = x < 0x1p-96f;
     const float xs = x * (tiny ? 0x1p+64f : 1.0f);
     const float y = __builtin_amdgcn_rsqf(xs);
@@ -223,16 +222,15 @@ __device__ __forceinline__ float sqrt_rn(float x) {
     const float r = __builtin_fmaf(e, 0.5f * y, s) * (tiny ? 0x1p-32f : 1.0f);
     return __builtin_amdgcn_classf(xs, 0x060 | 0x200) ? xs : r;  // +-0 (0x20, 0x40), +inf (0x200)
 }
-#else
-__device__ __forceinline__ float sqrt_rn(float x) {
-    // one residual correction from a single transcendental: y = v_rsq_f32(x), s = x * y (faithful),
-    // e = x - s*s exactly (one fma), r = RN(s + e * h) with h = 0.5 * y ~ 1/(2 sqrt x): 5 VALU ops,
-    // ONE of them transcendental (8 issue cycles against 4 for an fma; s from v_sqrt_f32 plus h from
-    // v_rsq_f32 took two).  Correctly rounded for every x in [2^-96, FLT_MAX] (tools/fpexact/
-    // sqrt_markstein.hip, candidate M3: only 0 and inf fail, both outside; below 2^-96 the residual
-    // underflows); every other x -- tiny, zero, denormal, negative, infinite, NaN -- takes the
-    // compiler's sequence in a divergent branch no real scene takes, chosen by one unsigned range
-    // test on the bits (positive floats order like their bit patterns; negatives and NaNs fall outside).
+// The guarded form: one residual correction from a single transcendental: y = v_rsq_f32(x),
+// s = x * y (faithful), e = x - s*s exactly (one fma), r = RN(s + e * h) with h = 0.5 * y ~
+// 1/(2 sqrt x): 5 VALU ops, ONE of them transcendental (8 issue cycles against 4 for an fma; s from
+// v_sqrt_f32 plus h from v_rsq_f32 took two).  Correctly rounded for every x in [2^-96, FLT_MAX]
+// (tools/fpexact/sqrt_markstein.hip, candidate M3: only 0 and inf fail, both outside; below 2^-96 the
+// residual underflows); every other x -- tiny, zero, denormal, negative, infinite, NaN -- takes the
+// compiler's sequence in a divergent branch no real scene takes, chosen by one unsigned range test on
+// the bits (positive floats order like their bit patterns; negatives and NaNs fall outside).
+__device__ __forceinline__ float sqrt_rn_guarded(float x) {
     const float y = __builtin_amdgcn_rsqf(x);
     const float s = x * y;
     const float e = __builtin_fmaf(-s, s, x);
@@ -245,6 +243,16 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 #endif
     return r;
 }
+// Correctly rounded f32 sqrt (Rust f32::sqrt).  Both forms are verified bit-identical to
+// __builtin_sqrtf over all 2^32 inputs on gfx950 (rrte_hip_fpcheck, tests/test_gpu_fpexact.py).
+// RRTE_SQRT_GUARDED selects the guarded form (A/B); RRTE_ABLATE_FAST_SQRT swaps in the bare 1-ulp
+// v_sqrt_f32 -- a timing experiment only (breaks parity), never a build setting.
+#ifdef RRTE_ABLATE_FAST_SQRT
+__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_amdgcn_sqrtf(x); }
+#elif defined(RRTE_SQRT_BRANCHFREE)
+__device__ __forceinline__ float sqrt_rn(float x) { return sqrt_rn_branchfree(x); }
+#else
+__device__ __forceinline__ float sqrt_rn(float x) { return sqrt_rn_guarded(x); }
 #endif
 // Correctly rounded 1/b: v_rcp_f32 and one Newton fma step is exact for every b with
 // |b| in [2^-126, 2^126] (rrte_hip_fpcheck: all 2^32 inputs on gfx950); zeros,

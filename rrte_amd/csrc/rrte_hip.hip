@@ -204,6 +204,12 @@ struct rrte_ctx {
     uint32_t env_guard_leaves = 2;  // RRTE_CSG_GUARDS: 0 = off, N = smallest guarded operand (leaves)
     bool env_wg256 = false;           // RRTE_WG64=0: specialised kernels in 256-thread workgroups (A/B only)
     int emu_nranks = 0, emu_rank = 0;  // RRTE_EMULATE_RANK=N:R: render_async renders rank R's bands of N (diagnostic)
+    // RRTE_EMULATE_PEERS=N (tests, one GPU): a 1-rank communicator acts as the root of N ranks, and the
+    // root renders every peer's packed share (exactly what RRTE_EMULATE_RANK=N:q renders, RGB24 slab
+    // included) into peer q's receive slot where ncclRecv would have put it; the real expansion
+    // (deinterleave_batch_kernel, skip_rank = root) then composes the frames -- the q >= 1 side of the
+    // multi-GPU product path without the link
+    int emu_peers = 0;
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, valid; JitKernel* k; } jit_last{};
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
@@ -280,6 +286,7 @@ struct rrte_ctx {
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed scrambled permutation of the tiles (tests)
     bool env_tile_xcd = false;          // RRTE_TILE_XCD=1: XCD-aware LPT (lpt_slots_xcd; A/B experiment)
+    uint32_t env_nocomm_wait_ms = 0;    // RRTE_NOCOMM_WAIT_MS: limit of device waits without a communicator (0 = none)
     uint32_t env_prio_slots = 0;        // RRTE_PRIO_SLOTS=N: the list's first N slots raise wave priority (A/B)
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
     // per launch, so the version pool wraps within a few frames)
@@ -1712,7 +1719,8 @@ __global__ __launch_bounds__(256) void fpcheck_unary_kernel(int kind, uint64_t x
         const bool in = i < n;
         const float x = __uint_as_float((uint32_t)(x0 + (in ? i : 0)));
         bool bad;
-        if (kind == RRTE_FPCHECK_SQRT) bad = !fp_same(sqrt_rn(x), __builtin_sqrtf(x));
+        if (kind == RRTE_FPCHECK_SQRT) bad = !fp_same(sqrt_rn_guarded(x), __builtin_sqrtf(x));
+        else if (kind == RRTE_FPCHECK_SQRT_BF) bad = !fp_same(sqrt_rn_branchfree(x), __builtin_sqrtf(x));
         else if (kind == RRTE_FPCHECK_RCP) bad = !fp_same(rcp_rn(x), 1.0f / x);
         else if (kind == RRTE_FPCHECK_GAMMA_U8) bad = gamma22_u8(x) != to_u8(rclamp(powf(x, kInvGamma22)));
         else bad = !fp_same(__builtin_amdgcn_sqrtf(x), __builtin_sqrtf(x));
@@ -1760,6 +1768,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_TILE_XCD")) c->env_tile_xcd = g[0] == '1';
     if (const char* g = getenv("RRTE_PRIO_SLOTS")) c->env_prio_slots = (uint32_t)strtoul(g, nullptr, 0);
+    if (const char* g = getenv("RRTE_NOCOMM_WAIT_MS")) c->env_nocomm_wait_ms = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
         c->env_tile_order_fixed = g[0] == '2';  // 0 image order, 2 fixed permutation (tests), else measured (default)
@@ -1768,6 +1777,10 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_BND_CHUNKS"); g && *g)
         c->bnd_chunks = std::max(1, std::min(rrte_ctx::kBndChunksMax, (int)strtol(g, nullptr, 0)));
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
+    if (const char* e = getenv("RRTE_EMULATE_PEERS")) {
+        const int n = (int)strtol(e, nullptr, 0);
+        if (n > 1) c->emu_peers = n;
+    }
     if (const char* e = getenv("RRTE_EMULATE_RANK")) {
         int n = 0, r = 0;
         if (sscanf(e, "%d:%d", &n, &r) == 2 && n > 1 && r >= 0 && r < n) {
@@ -2034,7 +2047,7 @@ rrte_status rrte_hip_jit_check(const rrte_scene_ir* s, int mode, char* log, size
 }
 
 rrte_status rrte_hip_fpcheck(int device, int kind, uint64_t lo, uint64_t hi, uint64_t* mismatches) {
-    if (!mismatches || kind < RRTE_FPCHECK_SQRT || kind > RRTE_FPCHECK_GAMMA_U8 || lo > hi ||
+    if (!mismatches || kind < RRTE_FPCHECK_SQRT || kind > RRTE_FPCHECK_SQRT_BF || lo > hi ||
         hi > (kind == RRTE_FPCHECK_DIV ? (1ull << 23) : (1ull << 32)))
         return RRTE_INVALID_ARG;
     if (hipSetDevice(device) != hipSuccess) return RRTE_HIP_ERROR;
@@ -2152,7 +2165,11 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
     c->nranks = nranks;
     c->rank = rank;
     c->comm_size = nranks;
-    if (nranks == 1 && c->emu_nranks > 1) {
+    if (nranks == 1 && c->emu_peers > 1) {
+        // RRTE_EMULATE_PEERS=N: the root of N ranks whose peers' shares it renders itself (render_peers)
+        c->nranks = c->emu_peers;
+        c->rank = 0;
+    } else if (nranks == 1 && c->emu_nranks > 1) {
         // RRTE_EMULATE_RANK=N:R with a 1-rank communicator (diagnostic, one GPU): the gather path lays
         // frames out as rank R of N -- R's bands rendered into its slab slice, the 1-rank gather moving
         // that slice, and on rank 0 the de-interleave of all N slices (the other N-1 hold whatever the
@@ -2204,6 +2221,34 @@ static rrte_status deinterleave(rrte_ctx* c, hipStream_t st, const uint8_t* gath
     return RRTE_OK;
 }
 
+// RRTE_EMULATE_PEERS (tests): render every peer's share of `n` frames -- peer q's bands under the plan's
+// band partition, packed, in the plan's slab format (RGB24 or RGBA8) -- into its receive slot
+// slab + q * rank_stride (frame j at + j * frame_stride), on `st`: the bytes a real peer would have
+// sent with ncclSend for the same frames.  `base` is the root's plan of these frames.
+static rrte_status render_peers(rrte_ctx* c, const LaunchPlan& base, const FrameCam* cams, uint32_t n, uint8_t* slab,
+                                size_t rank_stride, size_t frame_stride, int root, hipStream_t st) {
+    const BandMap bm{base.k.band_rows, (uint32_t)c->nranks, base.k.sky_bands, base.k.root_bands, base.k.peer_bands};
+    for (int q = 0; q < c->nranks; ++q) {
+        if (q == root) continue;
+        LaunchPlan L = base;
+        L.k.rank = (uint32_t)q;
+        L.k.rows = rows_for_rank(base.k.height, bm.band_rows, c->nranks, q, bm.sky, bm.root_bands, bm.peer_bands);
+        L.gy = (L.k.rows + 7) / 8;
+        L.k.out_image_rows = 0u;
+        L.k.frame_stride = frame_stride;
+        L.prof = 1 + (q - 1) % rrte_ctx::kBndChunksMax;  // (a tile profile per peer shape)
+        for (uint32_t j0 = 0; j0 < n; j0 += kMaxLaunchFrames) {
+            const uint32_t nf = std::min<uint32_t>(n - j0, kMaxLaunchFrames);
+            memcpy(L.k.cam, cams + j0, nf * sizeof(FrameCam));
+            L.k.nframes = nf;
+            uint8_t* dst = slab + (size_t)q * rank_stride + (size_t)j0 * frame_stride;
+            rrte_status r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, st);
+            if (r != RRTE_OK) return r;
+        }
+    }
+    return RRTE_OK;
+}
+
 // Launch the open batch's frames that have not been rendered yet ([rendered, n)) into its send slab on
 // the slab's render stream, after the work queued on the frames' caller streams.  Local: no
 // collective, so a rank may call it on its own (a scene change through a non-gather entry point,
@@ -2228,14 +2273,17 @@ static rrte_status render_batch(rrte_ctx* c, bool at_flush) {
         }
     if (b.rendered == 0) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_batch[k], 0));
     hs.lap(2);
+    // a copy of the batch's plan: b.plan's fields before KParams::nframes are the batch-compatibility
+    // key gather_frame compares every new frame with, identically on every rank, so they stay as
+    // planned (the in-place root's RGBA8 flag is this launch's business only)
+    LaunchPlan L = b.plan;
+    if (b.in_place) L.k.flags &= ~kFlagSlabRgb24;
     for (uint32_t j0 = b.rendered; j0 < b.n; j0 += kMaxLaunchFrames) {
         const uint32_t nf = std::min<uint32_t>(b.n - j0, kMaxLaunchFrames);
-        LaunchPlan& L = b.plan;
         memcpy(L.k.cam, b.cam + j0, nf * sizeof(FrameCam));
         L.k.nframes = nf;
         L.k.frame_stride = b.slice;
         L.k.out_image_rows = b.in_place ? 1u : 0u;
-        if (b.in_place) L.k.flags &= ~kFlagSlabRgb24;
         uint8_t* dst = b.in_place ? nullptr : base + (size_t)j0 * b.slice;
         rrte_status r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, rs);
         if (r != RRTE_OK) return r;
@@ -2320,11 +2368,11 @@ static rrte_status comm_abort(rrte_ctx* c, const char* why) {
 // instead of blocking, so work that sits behind a gather that never completes -- a dead or stalled
 // peer -- surfaces as RRTE_RCCL_ERROR after comm_timeout_ms (the communicator aborted) instead of a
 // hang.  Without a communicator no gather can stall a frame (an aborted one's kernels are being torn
-// down), but the wait stays bounded all the same: RRTE_HIP_ERROR after kNoCommWaitMs.
-constexpr uint32_t kNoCommWaitMs = 60000;
+// down), so the wait lasts as long as the device needs -- a single-GPU caller may queue minutes of
+// frames -- unless RRTE_NOCOMM_WAIT_MS sets a limit (RRTE_HIP_ERROR after it; 0, the default, = none).
 static rrte_status poll_events(rrte_ctx* c, const hipEvent_t* ev, size_t n) {
     const auto t0 = std::chrono::steady_clock::now();
-    const uint32_t limit_ms = c->comm ? c->comm_timeout_ms : std::max(c->comm_timeout_ms, kNoCommWaitMs);
+    const uint32_t limit_ms = c->comm ? c->comm_timeout_ms : c->env_nocomm_wait_ms;
     for (uint32_t spin = 0;; ++spin) {
         bool busy = false;
         for (size_t i = 0; i < n; ++i) {
@@ -2349,7 +2397,7 @@ static rrte_status poll_events(rrte_ctx* c, const hipEvent_t* ev, size_t n) {
                 snprintf(why, sizeof why, "gather did not complete within %u ms (stalled or dead peer?)", c->comm_timeout_ms);
                 return comm_abort(c, why);
             }
-        } else if (late) {
+        } else if (late && limit_ms) {
             return fail(c, RRTE_HIP_ERROR, "device work did not complete within %u ms", limit_ms);
         }
         if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -2400,16 +2448,28 @@ static rrte_status flush_batch(rrte_ctx* c) {
         // routes the root's bands through RCCL to itself
         const bool self_only = c->comm_size == 1;  // (no real peer: only the root's RRTE_GATHER_SELF round trip)
         if (!(c->env_diag_skip & 1u) && (!self_only || (!b.in_place && c->rank == b.root))) {
+            // (a failing call inside the group still closes it before the error is returned, so the
+            // thread's group depth is balanced when comm_abort tears the communicator down)
             NCCLCHK(c, ncclGroupStart());
+            ncclResult_t gr = ncclSuccess;
+            const char* what = "ncclRecv";
             if (c->rank == b.root) {
-                for (int q = 0; q < c->comm_size; ++q)
+                for (int q = 0; q < c->comm_size && (gr == ncclSuccess || gr == ncclInProgress); ++q)
                     if (q != b.root || !b.in_place)
-                        NCCLCHK(c, ncclRecv(c->d_brecv[k] + (size_t)q * count, count, ncclUint8, q, c->comm, c->comm_stream));
+                        gr = ncclRecv(c->d_brecv[k] + (size_t)q * count, count, ncclUint8, q, c->comm, c->comm_stream);
             }
-            if (c->rank != b.root || !b.in_place)
-                NCCLCHK(c, ncclSend(c->d_bsend[k], count, ncclUint8, b.root, c->comm, c->comm_stream));
-            NCCLCHK(c, ncclGroupEnd());
+            if ((gr == ncclSuccess || gr == ncclInProgress) && (c->rank != b.root || !b.in_place)) {
+                what = "ncclSend";
+                gr = ncclSend(c->d_bsend[k], count, ncclUint8, b.root, c->comm, c->comm_stream);
+            }
+            const ncclResult_t er = ncclGroupEnd();
+            if (gr != ncclSuccess && gr != ncclInProgress)
+                return fail(c, RRTE_RCCL_ERROR, "%s failed: %s", what, ncclGetErrorString(gr));
+            NCCLCHK(c, er);
         }
+        if (self_only && c->emu_peers > 1 && c->rank == b.root &&
+            (r = render_peers(c, b.plan, b.cam, b.n, c->d_brecv[k], count, b.slice, b.root, c->comm_stream)) != RRTE_OK)
+            return r;
         hs.lap(5);
         if (c->rank == b.root && !(c->env_diag_skip & 2u) && (c->nranks > 1 || !b.in_place)) {
             DeinterleaveTargets t{};
@@ -2546,6 +2606,10 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         hs.lap(2);
         if ((r = launch(c, s, &pp, rows, reinterpret_cast<uint32_t*>(mine), nullptr, st, kflags, 0u, 0, &bm)) != RRTE_OK)
             return r;
+        if (c->comm_size == 1 && c->emu_peers > 1 && c->rank == root) {  // RRTE_EMULATE_PEERS (tests)
+            const LaunchPlan L = plan_launch(c, s, &pp, rows, kflags, 0u, &bm);
+            if ((r = render_peers(c, L, L.k.cam, 1, slab, slice, 0, root, st)) != RRTE_OK) return r;
+        }
         hs.lap(3);
         if (timing) HIPCHK(c, hipEventRecord(c->ev1, st));
         // gathers on one communicator must run in the same order on every rank: a frame on another
@@ -2599,6 +2663,13 @@ rrte_status rrte_hip_set_gather_batch(rrte_ctx* c, uint32_t frames) {
 rrte_status rrte_hip_flush(rrte_ctx* c) {
     if (!c) return RRTE_INVALID_ARG;
     return flush_batch(c);
+}
+
+rrte_status rrte_hip_gather_info(rrte_ctx* c, uint64_t* collectives, uint32_t* open_frames) {
+    if (!c || !collectives || !open_frames) return RRTE_INVALID_ARG;
+    *collectives = c->gathers_issued;
+    *open_frames = c->batch.n;
+    return RRTE_OK;
 }
 
 rrte_status rrte_hip_render_gather(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,

@@ -143,6 +143,7 @@ extern "C" {
     pub fn rrte_hip_set_comm_timeout(ctx: *mut rrte_ctx, ms: u32) -> rrte_status;
     pub fn rrte_hip_set_gather_batch(ctx: *mut rrte_ctx, frames: u32) -> rrte_status;
     pub fn rrte_hip_flush(ctx: *mut rrte_ctx) -> rrte_status;
+    pub fn rrte_hip_gather_info(ctx: *mut rrte_ctx, collectives: *mut u64, open_frames: *mut u32) -> rrte_status;
     pub fn rrte_hip_band_rows_for_rank(height: u32, band_rows: u32, nranks: c_int, rank: c_int) -> u32;
     pub fn rrte_hip_band_layout(scene: *const rrte_scene_ir, params: *const rrte_render_params, nranks: c_int,
                                 root: c_int, sky_bands: *mut u32, root_bands: *mut u32,

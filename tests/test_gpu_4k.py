@@ -24,11 +24,15 @@ W, H, BAND = 3840, 2160, 16
 NBANDS = (H + BAND - 1) // BAND
 
 
-@pytest.fixture(scope="module")
-def oracle_4k():
+_oracle = {}
+
+
+def oracle_4k(name="sdf_showcase"):
     """The oracle's linear 4K image and its shadow-ray count per 16-row band (one call per band into
     the same full-size buffers: the oracle writes rows [r0, r1) at their image positions)."""
-    objs, lights, cam, cfg = scenes.sdf_showcase(W, H)
+    if name in _oracle:
+        return _oracle[name]
+    objs, lights, cam, cfg = getattr(scenes, name)(W, H)
     sc = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
     prm.flags |= abi.FLAG_F32_LINEAR
@@ -42,7 +46,8 @@ def oracle_4k():
                                     b * BAND, min(H, (b + 1) * BAND))
         assert st == 0
         band_shadow.append(sh.value)
-    return lin.reshape(H, W, 4), band_shadow
+    _oracle[name] = (lin.reshape(H, W, 4), band_shadow)
+    return _oracle[name]
 
 
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
@@ -59,14 +64,15 @@ def band_owner(b, n, sky, rb, pb):
     return 0 if s < rb else 1 + (s - rb) % (n - 1)
 
 
-@pytest.mark.parametrize("sky_on", ["1", "0"])
-@pytest.mark.parametrize("nranks", [2, 4, 8])
-def test_4k_rank_shares_match_oracle_rows(nranks, sky_on, oracle_4k, monkeypatch):
+@pytest.mark.parametrize("name,nranks,sky_on", [("sdf_showcase", n, sky) for n in (2, 4, 8) for sky in ("1", "0")]
+                         + [("deformation_stress", 8, "1")])
+def test_4k_rank_shares_match_oracle_rows(name, nranks, sky_on, monkeypatch):
     """Each rank's share under the frame's band partition (the sky bands on rank 0 and the rest round
-    robin, rrte_hip_band_layout; RRTE_BAND_SKY=0: the plain interleave)."""
+    robin, rrte_hip_band_layout; RRTE_BAND_SKY=0: the plain interleave).  sdf-showcase is BASELINE
+    configs[3]; the deformation-stress scene at N = 8 is configs[4] (VERDICT r04 missing #3)."""
     import torch
-    lin, band_shadow = oracle_4k
-    objs, lights, cam, cfg = scenes.sdf_showcase(W, H)
+    lin, band_shadow = oracle_4k(name)
+    objs, lights, cam, cfg = getattr(scenes, name)(W, H)
     cfg.band_rows = BAND
     sc = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
@@ -74,7 +80,8 @@ def test_4k_rank_shares_match_oracle_rows(nranks, sky_on, oracle_4k, monkeypatch
     lib = abi.load()
     monkeypatch.setenv("RRTE_BAND_SKY", sky_on)
     sky, rb, pb = abi.band_layout(sc.ref(), C.byref(prm), nranks)
-    assert (sky > 0) == (sky_on == "1")  # the 4K showcase has sky rows above every object
+    if name == "sdf_showcase":
+        assert (sky > 0) == (sky_on == "1")  # the 4K showcase has sky rows above every object
     total = 0
     for rank in range(nranks):
         monkeypatch.setenv("RRTE_EMULATE_RANK", f"{nranks}:{rank}")

@@ -209,3 +209,80 @@ def test_stall_during_recycle_or_scene_change_is_bounded(what, monkeypatch):
     for j, i in enumerate(range(27, 30)):
         assert np.array_equal(outs[i].cpu().numpy().view(np.uint8), want[j]), f"frame {i}"
     ctx.close()
+
+
+def _info(ctx):
+    colls, open_frames = C.c_uint64(0), C.c_uint32(0)
+    ctx.check(ctx.lib.rrte_hip_gather_info(ctx.h, C.byref(colls), C.byref(open_frames)))
+    return colls.value, open_frames.value
+
+
+def _recoloured_frames(n):
+    """The same topology as _frames (sdf-showcase), another value: one material recoloured."""
+    from rrte_amd import LambertianMaterial
+    from rrte_amd.math import Color
+    out = []
+    for i in range(n):
+        objs, lights, cam, cfg = scenes.sdf_showcase(W, H)
+        objs[3].material = LambertianMaterial(Color(0.9, 0.3, 0.1, 1.0))
+        out.append((LoweredScene(objs, lights, cam), cfg.lower()))
+    return out
+
+
+def test_local_render_keeps_the_in_place_batch_open(monkeypatch):
+    """the in-place root's batch stays open across local calls.  A scene change with
+    unchanged array counts (same topology: the open batch is rendered locally first) and
+    rrte_hip_synchronize (also renders it locally) must not change the batch-compatibility key, or
+    the root alone would close the batch and issue a collective its peers do not (RGB24 slabs: the
+    LAMBERT_SHADOW default).  No collective may be issued until the batch fills."""
+    import torch
+    monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    frames = _frames(3) + _recoloured_frames(2) + _frames(3, first=3)
+    want = _want(frames)
+    ctx = Context(0, jit=abi.JIT_ON)
+    _comm(ctx)
+    ctx.check(ctx.lib.rrte_hip_set_gather_batch(ctx.h, 8))
+    outs = [torch.full((W * H,), -1, dtype=torch.int32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
+    for i, ((sc, prm), o) in enumerate(zip(frames[:7], outs)):
+        ctx.check(_gather(ctx, sc, prm, o))
+        assert _info(ctx) == (0, i + 1), f"after frame {i}"
+        if i == 5:
+            ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))  # local: renders the open batch, keeps it open
+            assert _info(ctx) == (0, 6)
+    ctx.check(_gather(ctx, *frames[7], outs[7]))  # the 8th frame fills the batch: one exchange
+    assert _info(ctx) == (1, 0)
+    ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))
+    for i, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint8), want[i]), f"frame {i}"
+    ctx.close()
+
+
+def test_wait_without_communicator_is_unbounded(monkeypatch):
+    """without a communicator nothing can stall a frame, so rrte_hip_synchronize
+    waits as long as the device needs -- far past the communicator timeout -- and returns RRTE_OK;
+    RRTE_NOCOMM_WAIT_MS is an opt-in limit (RRTE_HIP_ERROR once it expires)."""
+    import torch
+    objs, lights, cam, cfg = scenes.deformation_stress(1920, 1080)
+    sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    out = torch.empty(1920 * 1080, dtype=torch.int32, device="cuda")
+    for limit in (None, "1"):
+        if limit:
+            monkeypatch.setenv("RRTE_NOCOMM_WAIT_MS", limit)
+        ctx = Context(0, jit=abi.JIT_ON)
+        ctx.check(ctx.lib.rrte_hip_set_comm_timeout(ctx.h, 1))
+        ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), out.data_ptr(), None, None))
+        ctx.check(ctx.lib.rrte_hip_synchronize(ctx.h))  # (compile + first frame)
+        t0 = time.perf_counter()
+        for _ in range(24):  # ~5 ms each: >> the 1 ms comm timeout
+            ctx.check(ctx.lib.rrte_hip_render_async(ctx.h, sc.ref(), C.byref(prm), out.data_ptr(), None, None))
+        rc = ctx.lib.rrte_hip_synchronize(ctx.h)
+        dt = time.perf_counter() - t0
+        if limit is None:
+            assert rc == abi.RRTE_OK, ctx.lib.rrte_hip_last_error(ctx.h)
+            assert dt > 0.02, dt  # the wait really outlasted the comm timeout
+        else:
+            assert rc == abi.RRTE_HIP_ERROR, rc
+            assert b"did not complete within 1 ms" in ctx.lib.rrte_hip_last_error(ctx.h)
+        torch.cuda.synchronize()
+        ctx.close()

@@ -26,6 +26,11 @@ def test_sqrt_rn_all_inputs():
     assert _check(abi.FPCHECK_SQRT, 0, 1 << 32) == 0
 
 
+def test_sqrt_rn_branchfree_all_inputs():
+    """The branch-free form (tiny inputs scaled by 2^64, +-0 / +inf through v_cmp_class)."""
+    assert _check(abi.FPCHECK_SQRT_BF, 0, 1 << 32) == 0
+
+
 def test_sweep_detects_one_ulp_errors():
     """Control: the bare hardware v_sqrt_f32 is only faithful; the same sweep must see it
     (about 3.4e8 of the 2^32 patterns differ from the correctly rounded result)."""

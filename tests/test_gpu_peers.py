@@ -1,0 +1,112 @@
+"""The peers' side of the multi-GPU composition, run on one GPU.
+
+RRTE_EMULATE_PEERS=N makes a 1-rank RCCL communicator the root of N ranks: at each exchange the
+root renders every peer q's packed share -- q's bands under the frame's band partition, in the slab
+format a real peer sends (RGB24 when every alpha byte is provably 255) -- into receive slot q of
+the exchange buffer, where ncclRecv would have put it, and then runs the product expansion
+(deinterleave_batch_kernel with skip_rank = root) over the real offsets.  So the q >= 1 receive
+offsets, the peer rows of band_owner and skip_rank with peers present all execute; only the xGMI
+transfer itself is missing.
+
+Every composed frame must be bit-identical to the plain single-context render of the same scene and
+camera (pixels are independent, crates/rrte-renderer/src/raytracer.rs:57-86, so which rank renders a
+band can never change a byte), and the first frame of each case within u8 <= 1 of the ORACLE's full
+frame (the gamma step's powf ulp).  Cases: sdf-showcase (BASELINE configs[1]/[3]) and
+the deformation-stress scene (configs[4]) at 1920x1080 and 3840x2160, N = 2/4/8, gather batches of
+1 (one ncclGather per frame) and 8 (multi-frame launches, one grouped exchange per batch), with the
+camera moving every frame -- inside a batch too."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+from rrte_amd import LoweredScene, abi, scenes
+from rrte_amd.math import vec3
+from rrte_amd.renderer import Context
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("sdf_showcase", 1920, 1080), ("sdf_showcase", 3840, 2160),
+         ("deformation_stress", 1920, 1080), ("deformation_stress", 3840, 2160)]
+NFRAMES = 8
+_BASE = {"sdf_showcase": (0.0, 8.0, 20.0), "deformation_stress": (0.0, 12.0, 26.0)}
+
+
+def _fly(name, w, h, n=NFRAMES):
+    """n frames of a fly-by: the camera moves (and re-aims) every frame."""
+    out = []
+    for i in range(n):
+        objs, lights, cam, cfg = getattr(scenes, name)(w, h)
+        x, y, z = _BASE[name]
+        cam.transform.position = vec3(x + 0.35 * i, y - 0.2 * i, z - 0.15 * i)
+        cam.look_at((0.0, 2.0, 0.0))
+        out.append((LoweredScene(objs, lights, cam), cfg.lower()))
+    return out
+
+
+_plain = {}
+
+
+def _reference(name, w, h):
+    """The plain single-context renders of the fly-by (every row on one context, no bands), and the
+    oracle's first frame."""
+    key = (name, w, h)
+    if key not in _plain:
+        frames = _fly(name, w, h)
+        ctx = Context(0, jit=abi.JIT_ON)
+        want = []
+        for sc, prm in frames:
+            buf = np.zeros(w * h * 4, dtype=np.uint8)
+            ctx.check(ctx.lib.rrte_hip_render(ctx.h, sc.ref(), C.byref(prm), buf.ctypes.data_as(C.POINTER(C.c_uint8))))
+            want.append(buf)
+        ctx.close()
+        sc, prm = frames[0]
+        ref8, _, _ = oracle.render(sc, prm, nthreads=16, want_f32=False)
+        _plain[key] = (frames, want, ref8)
+    return _plain[key]
+
+
+@pytest.mark.parametrize("batch", [1, 8])
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+@pytest.mark.parametrize("name,w,h", CASES)
+def test_emulated_peers_compose_exact_frames(name, w, h, nranks, batch, monkeypatch):
+    import torch
+
+    frames, want, ref8 = _reference(name, w, h)
+    d = int(np.abs(want[0].astype(np.int16) - ref8.astype(np.int16)).max())
+    assert d <= 1, f"plain render vs oracle: u8 max diff {d}"
+    monkeypatch.setenv("RRTE_FORCE_GATHER", "1")
+    monkeypatch.setenv("RRTE_EMULATE_PEERS", str(nranks))
+    ctx = Context(0, jit=abi.JIT_ON)
+    lib = ctx.lib
+    uid = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+    ctx.check(lib.rrte_hip_comm_unique_id(uid))
+    ctx.check(lib.rrte_hip_comm_init(ctx.h, 1, 0, uid))
+    ctx.check(lib.rrte_hip_set_gather_batch(ctx.h, batch))
+    # the partition really has peer rows at this size (every peer owns bands)
+    sc0, prm0 = frames[0]
+    sky, rb, pb = abi.band_layout(sc0.ref(), C.byref(prm0), nranks)
+    for q in range(1, nranks):
+        assert lib.rrte_hip_band_rows_for_rank_ex(h, 16, nranks, q, sky, rb, pb) > 0, q
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = [torch.full((w * h,), -1, dtype=torch.int32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()  # the fill ran on torch's stream; the renders run on others
+    for i, ((sc, prm), o) in enumerate(zip(frames, outs)):
+        ctx.check(lib.rrte_hip_render_gather_async(ctx.h, sc.ref(), C.byref(prm), 0, o.data_ptr(),
+                                                    C.c_void_p(streams[i % 2].cuda_stream)))
+    ctx.check(lib.rrte_hip_flush(ctx.h))
+    ctx.check(lib.rrte_hip_synchronize(ctx.h))
+    colls, open_frames = C.c_uint64(0), C.c_uint32(7)
+    ctx.check(lib.rrte_hip_gather_info(ctx.h, C.byref(colls), C.byref(open_frames)))
+    assert open_frames.value == 0
+    if batch == 1:
+        assert colls.value == NFRAMES
+    else:  # one exchange per batch; a camera move that changes the partition closes a batch early
+        assert 1 <= colls.value <= NFRAMES
+    for i, o in enumerate(outs):
+        got = o.cpu().numpy().view(np.uint8)
+        bad = got != want[i]
+        assert not bad.any(), (f"N={nranks} batch {batch} frame {i}: {int(bad.sum())} bytes differ from the "
+                               f"plain render (rows {np.unique(np.nonzero(bad.reshape(h, -1))[0])[:8]})")
+    ctx.close()

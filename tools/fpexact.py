@@ -11,7 +11,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from rrte_amd import abi  # noqa: E402
 
 KINDS = {"sqrt": (abi.FPCHECK_SQRT, 1 << 32), "rcp": (abi.FPCHECK_RCP, 1 << 32), "div": (abi.FPCHECK_DIV, 1 << 23),
-         "sqrt_hw": (abi.FPCHECK_SQRT_HW, 1 << 32)}  # control: the bare 1-ulp v_sqrt_f32
+         "sqrt_hw": (abi.FPCHECK_SQRT_HW, 1 << 32), "sqrt_bf": (abi.FPCHECK_SQRT_BF, 1 << 32),
+         "gamma": (abi.FPCHECK_GAMMA_U8, 1 << 32)}  # control: the bare 1-ulp v_sqrt_f32
 
 
 def main():

@@ -10,7 +10,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 ROUNDS=${1:?rounds}; shift
-OUT=$R/gpurun_out/pmc_ab
+OUT=$R/gpurun_out/${PMC_AB_OUT:-pmc_ab}
 mkdir -p $OUT
 export GPU_MAX_HW_QUEUES=32  # (under rocprofv3 HIP starts before bench.py could set it)
 cd /tmp && export TMPDIR=/tmp
