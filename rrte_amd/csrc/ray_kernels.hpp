@@ -35,15 +35,30 @@ struct MeshView {
     const uint32_t* __restrict__ perm;
 };
 
+// Scene features the generic kernel is compiled for (SceneView::kFeat): the host picks the smallest
+// precompiled variant whose features cover the scene (rrte_hip.hip generic_kernel), so a scene without
+// meshes, deformers or non-sphere analytic objects runs a kernel without their code -- fewer live
+// registers, a higher occupancy, no traversal stack in LDS.  Spheres are always compiled in.
+constexpr uint32_t kFeatMesh = 1u;      // RRTE_PRIM_MESH objects (BVH traversal, LDS stack)
+constexpr uint32_t kFeatDeform = 2u;    // SDF programs with deformers (bend, twist, taper, noise, wave)
+constexpr uint32_t kFeatAnalytic = 4u;  // plane, triangle, cube, cylinder, cone, capsule
+constexpr uint32_t kFeatSdf = 8u;       // SDF objects
+constexpr uint32_t kFeatAll = 15u;
+
 struct SceneView {
     static constexpr bool kStatic = false;
     static constexpr bool kTopo = false;
+    static constexpr uint32_t kFeat = kFeatAll;
     const DPrim* __restrict__ prims;
     const DMaterial* __restrict__ mats;
     const DLight* __restrict__ lights;
     const rrte_sdf_node* __restrict__ nodes;
     uint32_t num_prims, num_lights, num_materials;
     MeshView mesh;
+};
+template <uint32_t F>
+struct SceneViewF : SceneView {
+    static constexpr uint32_t kFeat = F;
 };
 
 // Loop over objects / lights: a plain loop for the runtime scene, compile-time
@@ -314,7 +329,7 @@ __device__ __forceinline__ f3 sdf_deform(G& g, uint32_t op, const uint32_t* __re
 // replace it, POP_POINT restores it).
 // (op and the integer arguments separately from the float arguments: a topology kernel has the
 // first two at compile time and reads the third.)
-template <class G>
+template <class G, bool DEFORM = true>
 __device__ __forceinline__ void sdf_node_step(G& g, uint32_t op, const uint32_t* iargs, const float* fargs, float* vs,
                                               f3* ps, uint32_t& sp, uint32_t& pp, f3& p) {
     if (op < 32) {
@@ -334,13 +349,15 @@ __device__ __forceinline__ void sdf_node_step(G& g, uint32_t op, const uint32_t*
         sp -= 2;
         vs[sp] = r;
         ++sp;
-    } else if (op < 96) {
-        ps[pp] = p;
-        ++pp;
-        p = sdf_deform(g, op, iargs, fargs, p);
-    } else {
-        --pp;
-        p = ps[pp];
+    } else if constexpr (DEFORM) {  // (a program of a scene without deformers has none: kFeatDeform)
+        if (op < 96) {
+            ps[pp] = p;
+            ++pp;
+            p = sdf_deform(g, op, iargs, fargs, p);
+        } else {
+            --pp;
+            p = ps[pp];
+        }
     }
 }
 
@@ -384,14 +401,15 @@ __device__ __forceinline__ bool sdf_guard(G& gp, uint32_t gop, const float* gf, 
 // wave-uniform (every lane runs the same program), so the stacks stay in
 // registers indexed by SGPR values.  A guarded operand is skipped when its
 // guard holds for the whole wave.
-struct SdfProgram {
+template <uint32_t F = kFeatAll>
+struct SdfProgramT {
     static constexpr bool kSmall = false;
     const rrte_sdf_node* __restrict__ nodes;
     uint32_t count;
     template <class G>
     __device__ __forceinline__ float eval(f3 p, G& g) const {
         float vs[RRTE_SDF_MAX_STACK];
-        f3 ps[RRTE_SDF_MAX_POINT_STACK];
+        f3 ps[(F & kFeatDeform) ? RRTE_SDF_MAX_POINT_STACK : 1];
         uint32_t sp = 0, pp = 0;
         for (uint32_t i = 0; i < count; ++i) {
             const uint32_t link = nodes[i].i[2];
@@ -401,7 +419,7 @@ struct SdfProgram {
                 i = link - 1u;  // continue after the op
                 continue;
             }
-            sdf_node_step(g, nodes[i].op, nodes[i].i, nodes[i].f, vs, ps, sp, pp, p);
+            sdf_node_step<G, (F & kFeatDeform) != 0u>(g, nodes[i].op, nodes[i].i, nodes[i].f, vs, ps, sp, pp, p);
         }
         return vs[0];
     }
@@ -410,6 +428,7 @@ struct SdfProgram {
         return eval(p, g);
     }
 };
+using SdfProgram = SdfProgramT<kFeatAll>;
 
 // Is the postfix program a convex, 1-Lipschitz function of p?  Convex leaves (exact SDFs of convex
 // solids -- the signed distance of a convex set is a supremum of affine functions -- and the prism's
@@ -1173,20 +1192,27 @@ template <bool NEED_HIT, class S, bool ANY = false>
 __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t_max,
                                              Hit& out) {
     const DPrim& pr = sc.prims[i];
-    switch (pr.kind) {
-    case RRTE_PRIM_SPHERE: return isect_sphere<NEED_HIT, ANY>(pr, r, t_min, t_max, out);
-    case RRTE_PRIM_PLANE: return isect_plane<NEED_HIT>(pr, r, t_min, t_max, out);
-    case RRTE_PRIM_TRIANGLE: return isect_triangle<NEED_HIT>(pr, r, t_min, t_max, out);
-    case RRTE_PRIM_CUBE: return isect_cube<NEED_HIT>(pr, r, t_min, t_max, out);
-    case RRTE_PRIM_CYLINDER: return isect_cylinder<NEED_HIT>(pr, r, t_min, t_max, out);
-    case RRTE_PRIM_CONE: return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
-    case RRTE_PRIM_CAPSULE: return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
-    case RRTE_PRIM_SDF:
-        return isect_sdf<NEED_HIT, SdfProgram, ANY>(pr, SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t_min,
-                                                    t_max, out);
-    case RRTE_PRIM_MESH: return isect_mesh<ANY>(pr, sc.mesh, r, t_min, t_max, out);
-    default: return false;
+    constexpr uint32_t F = S::kFeat;
+    // (a kind outside the variant's features cannot occur: the host picked the variant from the scene)
+    if (pr.kind == RRTE_PRIM_SPHERE) return isect_sphere<NEED_HIT, ANY>(pr, r, t_min, t_max, out);
+    if constexpr ((F & kFeatSdf) != 0u)
+        if (pr.kind == RRTE_PRIM_SDF)
+            return isect_sdf<NEED_HIT, SdfProgramT<F>, ANY>(pr, SdfProgramT<F>{sc.nodes + pr.sdf_first, pr.sdf_count},
+                                                            r, t_min, t_max, out);
+    if constexpr ((F & kFeatAnalytic) != 0u) {
+        switch (pr.kind) {
+        case RRTE_PRIM_PLANE: return isect_plane<NEED_HIT>(pr, r, t_min, t_max, out);
+        case RRTE_PRIM_TRIANGLE: return isect_triangle<NEED_HIT>(pr, r, t_min, t_max, out);
+        case RRTE_PRIM_CUBE: return isect_cube<NEED_HIT>(pr, r, t_min, t_max, out);
+        case RRTE_PRIM_CYLINDER: return isect_cylinder<NEED_HIT>(pr, r, t_min, t_max, out);
+        case RRTE_PRIM_CONE: return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
+        case RRTE_PRIM_CAPSULE: return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
+        default: break;
+        }
     }
+    if constexpr ((F & kFeatMesh) != 0u)
+        if (pr.kind == RRTE_PRIM_MESH) return isect_mesh<ANY>(pr, sc.mesh, r, t_min, t_max, out);
+    return false;
 }
 
 // Compile-time object index (scene-specialised kernel): only the object's
@@ -1257,10 +1283,24 @@ template <class S>
 __device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t,
                                               uint32_t sub, Hit& out) {
     const DPrim& pr = sc.prims[i];
-    if (pr.kind == RRTE_PRIM_SDF) sdf_hit_attributes(SdfProgram{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t, out);
-    else if (pr.kind == RRTE_PRIM_MESH) mesh_tri_hit(sc.mesh, sub, r, t_min, kInf, out);
-    else if (pr.kind == RRTE_PRIM_SPHERE) sphere_attributes(pr, r, t, out);
-    else intersect_at<true>(sc, i, r, t_min, kInf, out);
+    constexpr uint32_t F = S::kFeat;
+    if (pr.kind == RRTE_PRIM_SPHERE) {
+        sphere_attributes(pr, r, t, out);
+        return;
+    }
+    if constexpr ((F & kFeatSdf) != 0u) {
+        if (pr.kind == RRTE_PRIM_SDF) {
+            sdf_hit_attributes(SdfProgramT<F>{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t, out);
+            return;
+        }
+    }
+    if constexpr ((F & kFeatMesh) != 0u) {
+        if (pr.kind == RRTE_PRIM_MESH) {
+            mesh_tri_hit(sc.mesh, sub, r, t_min, kInf, out);
+            return;
+        }
+    }
+    if constexpr ((F & kFeatAnalytic) != 0u) intersect_at<true>(sc, i, r, t_min, kInf, out);
 }
 template <class S, uint32_t I>
 __device__ __forceinline__ void attributes_at(const S& sc, UC<I> ii, const Ray& r, float t_min, float t, uint32_t sub,
@@ -2118,12 +2158,18 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     }
 }
 
-// Generic kernel: the scene is read from HBM through wave-uniform (scalar) loads.
-template <int MODE, bool CULL>
-__global__ __launch_bounds__(kBlockThreads) void ray_kernel(KParams kp, SceneView sc, Cull cl, uint32_t* __restrict__ out_rgba8,
+// Generic kernel: the scene is read from HBM through wave-uniform (scalar) loads; F = the features
+// compiled in (kFeat*, a superset of the scene's).
+#ifndef RRTE_GENERIC_MINWAVES
+#define RRTE_GENERIC_MINWAVES 1
+#endif
+template <int MODE, bool CULL, uint32_t F = kFeatAll>
+__global__ __launch_bounds__(kBlockThreads, RRTE_GENERIC_MINWAVES) void ray_kernel(KParams kp, SceneView sc, Cull cl, uint32_t* __restrict__ out_rgba8,
                                                   float4* __restrict__ out_f32,
                                                   unsigned long long* __restrict__ counters) {
-    ray_kernel_body<MODE, SceneView, false, CULL>(kp, sc, cl, out_rgba8, out_f32, counters);
+    SceneViewF<F> s;
+    static_cast<SceneView&>(s) = sc;
+    ray_kernel_body<MODE, SceneViewF<F>, false, CULL>(kp, s, cl, out_rgba8, out_f32, counters);
 }
 
 // Root-side de-interleave after the RCCL gather: the gathered buffer holds, per rank (rank_stride

@@ -211,6 +211,8 @@ struct rrte_ctx {
     // multi-GPU product path without the link
     int emu_peers = 0;
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
+    uint32_t scene_feat = kFeatAll;  // the cached scene's features (kFeat*): its generic kernel variant
+    bool env_generic_all = false;    // RRTE_GENERIC_ALL=1: the all-features generic kernel for every scene (A/B, tests)
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, valid; JitKernel* k; } jit_last{};
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
     // topology kernels (jit.hip JitTopo): the cached scene's topology key and structural decisions, and
@@ -738,6 +740,19 @@ std::string topology_of(const std::vector<DPrim>& prims, const std::vector<DLigh
     return key;
 }
 
+// The features of a scene (kFeat*) that pick its generic kernel variant.
+uint32_t scene_features(const std::vector<DPrim>& prims, const std::vector<rrte_sdf_node>& nodes) {
+    uint32_t f = 0u;
+    for (const DPrim& p : prims) {
+        if (p.kind == RRTE_PRIM_MESH) f |= kFeatMesh;
+        else if (p.kind == RRTE_PRIM_SDF) f |= kFeatSdf;
+        else if (p.kind != RRTE_PRIM_SPHERE) f |= kFeatAnalytic;
+    }
+    for (const rrte_sdf_node& n : nodes)
+        if (n.op >= 64u) f |= kFeatDeform;  // deformers and their point pops
+    return f;
+}
+
 rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
     const size_t bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
     SceneKeyParts kparts;
@@ -839,6 +854,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     c->h_mats = mats;
     c->h_lights = lights;
     c->h_nodes = std::move(nodes);
+    c->scene_feat = scene_features(c->h_prims, c->h_nodes);
     c->value_edits = (!c->topo_key.empty() && tkey == c->topo_key) ? c->value_edits + 1 : 0;
     c->topo_key = std::move(tkey);
     c->topo = std::move(topo);
@@ -1551,6 +1567,21 @@ rrte_status finish_tile_order(rrte_ctx* c, const LaunchPlan& L, bool profile, hi
     return RRTE_OK;
 }
 
+// The generic kernel variant for a scene with features `need` (kFeat*): the first of the
+// precompiled feature sets F0, F1, F2 that covers it, else every feature (ray_kernels.hpp SceneView).
+template <int MODE, bool CULL, uint32_t F0, uint32_t F1, uint32_t F2>
+void launch_generic(uint32_t need, dim3 grid, dim3 block, hipStream_t st, const KParams& k, const SceneView& sv,
+                    const Cull& cl, uint32_t* d_rgba, float4* d_f32, unsigned long long* ctr) {
+    if ((need & ~F0) == 0u)
+        hipLaunchKernelGGL((ray_kernel<MODE, CULL, F0>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, ctr);
+    else if ((need & ~F1) == 0u)
+        hipLaunchKernelGGL((ray_kernel<MODE, CULL, F1>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, ctr);
+    else if ((need & ~F2) == 0u)
+        hipLaunchKernelGGL((ray_kernel<MODE, CULL, F2>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, ctr);
+    else
+        hipLaunchKernelGGL((ray_kernel<MODE, CULL, kFeatAll>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, ctr);
+}
+
 // Launch plan `L` (L.k.nframes frames) on `st`; the cached scene is the plan's.
 rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     if (L.gy == 0) return RRTE_OK;
@@ -1587,12 +1618,16 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
                  c->mesh_view};
     const KParams& k = L.k;
+    const uint32_t need = c->env_generic_all ? kFeatAll : c->scene_feat;
     if (L.mode == RRTE_MODE_REFCOMPAT)
-        hipLaunchKernelGGL((ray_kernel<RRTE_MODE_REFCOMPAT, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
+        launch_generic<RRTE_MODE_REFCOMPAT, false, 0u, kFeatAnalytic, kFeatSdf>(need, grid, block, st, k, sv, cl, d_rgba,
+                                                                             d_f32, c->d_counters);
     else if (L.cull)
-        hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, true>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
+        launch_generic<RRTE_MODE_LAMBERT_SHADOW, true, kFeatSdf, kFeatSdf | kFeatDeform, kFeatSdf | kFeatAnalytic>(
+            need, grid, block, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
     else
-        hipLaunchKernelGGL((ray_kernel<RRTE_MODE_LAMBERT_SHADOW, false>), grid, block, 0, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
+        launch_generic<RRTE_MODE_LAMBERT_SHADOW, false, 0u, kFeatAnalytic, kFeatSdf>(need, grid, block, st, k, sv, cl,
+                                                                                    d_rgba, d_f32, c->d_counters);
     HIPCHK(c, hipGetLastError());
     return finish_tile_order(c, L, profile, st);
 }
@@ -1768,6 +1803,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_TILE_XCD")) c->env_tile_xcd = g[0] == '1';
     if (const char* g = getenv("RRTE_PRIO_SLOTS")) c->env_prio_slots = (uint32_t)strtoul(g, nullptr, 0);
+    if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
     if (const char* g = getenv("RRTE_NOCOMM_WAIT_MS")) c->env_nocomm_wait_ms = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
