@@ -60,6 +60,9 @@ def parse():
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
                          "so one frame's tail overlaps the next frame's start (1 = strictly one after another); "
                          "default 4 on one GPU (tools/runs/r02_inflight.sh); N > 1: frames per gather batch, default 8")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="N > 1: caller streams the frames rotate over (each frame is launched at its call on its "
+                         "stream; frames in flight), independent of the gather batch (--inflight)")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
@@ -287,12 +290,12 @@ def main():
         cfg.jitter = "random"
     scene = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
-    # N > 1: frames are exchanged in batches of F (rrte_hip_set_gather_batch): each batch renders in
-    # multi-frame launches (8 frames per launch) on the library's render streams -- rank 0 writing its
-    # own bands straight into the frame buffers -- and ONE grouped ncclSend / ncclRecv per batch on its
-    # comm stream moves the peers' RGB24 rows to rank 0, which expands them.  Batches of
-    # 8 keep the last batch's exchange short at the driver's 20 steps.  Every frame is still composed
-    # on rank 0 inside the timed region (the last batch is flushed before its end).
+    # N > 1: every frame is launched at its call on one of --streams caller streams (frames in flight)
+    # -- rank 0 writing its own bands straight into the frame buffers, the peers into their send slabs
+    # -- and the frames are exchanged in batches of F (rrte_hip_set_gather_batch): ONE grouped
+    # ncclSend / ncclRecv per batch on the library's comm stream moves the peers' RGB24 rows to rank 0,
+    # which expands them.  Every frame is still composed on rank 0 inside the timed
+    # region (the last batch is flushed before its end).
     ctx = Context(local_rank, jit={"off": abi.JIT_OFF, "on": abi.JIT_ON, "auto": abi.JIT_AUTO}[args.jit])
     lib = ctx.lib
 
@@ -310,7 +313,8 @@ def main():
 
     W, H = args.width, args.height
     # dedicated (non-null) streams, one output buffer per frame in flight
-    streams = [torch.cuda.Stream(dev) for _ in range(F)]
+    streams = [torch.cuda.Stream(dev) for _ in range(max(F, args.streams) if gath else F)]
+    NS = max(1, min(args.streams, len(streams))) if gath else F  # caller streams the gather frames rotate over
     fulls = [torch.empty(W * H, dtype=torch.int32, device=dev) for _ in range(F)]
     full, stream = fulls[0], streams[0]
     torch.cuda.set_stream(stream)
@@ -325,9 +329,8 @@ def main():
     def step(i=0):
         j = i % F
         if gath:
-            # batched frames render on the library's own streams (multi-frame launches at the flush):
-            # one caller stream keeps the batch's dependency on its callers to one event
-            st = render_gather(h, sref, pref, 0, fptrs[j] if rank == 0 else None, sptrs[0])
+            # each frame launched at its call on caller stream i % NS; the exchange is batched
+            st = render_gather(h, sref, pref, 0, fptrs[j] if rank == 0 else None, sptrs[i % NS])
         else:
             st = render_async(h, sref, pref, fptrs[j], None, sptrs[j])
         if st:

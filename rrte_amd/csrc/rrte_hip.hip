@@ -145,6 +145,7 @@ struct rrte_ctx {
         uint32_t n = 0, cap = 0;             // frames planned into it / frames it was opened for
         uint32_t rendered = 0;               // frames [0, rendered) already launched into the send slab
         bool in_place = false;               // root: its bands rendered straight into the frames (RGBA8)
+        bool per_frame = false;              // each frame launched at its call (not at the batch's close)
         uint32_t width = 0, height = 0, band = 0;
         BandMap bm{};                        // the batch's band partition (a frame with another closes it)
         int root = 0;
@@ -213,6 +214,10 @@ struct rrte_ctx {
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
     uint32_t scene_feat = kFeatAll;  // the cached scene's features (kFeat*): its generic kernel variant
     bool env_generic_all = false;    // RRTE_GENERIC_ALL=1: the all-features generic kernel for every scene (A/B, tests)
+    // Batched gathers render each frame at its call (its own launch on the caller's stream: the root
+    // in place, a peer into its slot of the send slab) and only the exchange is batched; RRTE_BATCH_LAUNCH=1
+    // keeps round 4's multi-frame launches at the batch's close (A/B)
+    bool env_batch_launch = false;
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, valid; JitKernel* k; } jit_last{};
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
     // topology kernels (jit.hip JitTopo): the cached scene's topology key and structural decisions, and
@@ -1804,6 +1809,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_TILE_XCD")) c->env_tile_xcd = g[0] == '1';
     if (const char* g = getenv("RRTE_PRIO_SLOTS")) c->env_prio_slots = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
+    if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] == '1';
     if (const char* g = getenv("RRTE_NOCOMM_WAIT_MS")) c->env_nocomm_wait_ms = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
@@ -2468,13 +2474,22 @@ static rrte_status flush_batch(rrte_ctx* c) {
         b.n = b.nsrc = b.rendered = 0;
         return fail(c, RRTE_RCCL_ERROR, "gather batch dropped: %s", c->comm_failed ? c->comm_fail_msg.c_str() : "no communicator");
     }
-    rrte_status r = render_batch(c, true);
+    const bool launched_per_frame = b.per_frame;
+    rrte_status r = launched_per_frame ? RRTE_OK : render_batch(c, true);
     if (r != RRTE_OK) return comm_abort(c, ("batch render failed: " + c->err).c_str());
     HostSection hs(c);
     const int k = c->bslot;
     const size_t count = (size_t)b.n * b.slice;  // bytes per rank
     auto issue = [&]() -> rrte_status {
-        HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
+        if (launched_per_frame) {
+            // the frames rendered on their callers' streams: the exchange follows each of them
+            for (uint32_t i = 0; i < b.nsrc; ++i) {
+                HIPCHK(c, hipEventRecord(b.ev_src[i], b.src[i]));
+                HIPCHK(c, hipStreamWaitEvent(c->comm_stream, b.ev_src[i], 0));
+            }
+        } else {
+            HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
+        }
         if (c->last_gather_stream && c->last_gather_stream != c->comm_stream)
             HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->last_gather_ev, 0));
         hs.lap(4);
@@ -2598,6 +2613,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             b.bm = bm;
             b.plan = L;
             b.in_place = c->rank == root && !c->env_gather_self;
+            b.per_frame = !c->env_batch_launch;
             // every rank holds a receive slab too (the root's is the only one written)
             const size_t send = (size_t)b.cap * slice, recv = send * (size_t)c->nranks;
             if (c->cap_bsend[k] < send || c->cap_brecv[k] < recv) {
@@ -2616,7 +2632,24 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
         b.full[b.n] = static_cast<uint32_t*>(d_full);
         uint32_t i = 0;
         while (i < b.nsrc && b.src[i] != st) ++i;
-        if (i == b.nsrc) b.src[b.nsrc++] = st;
+        const bool new_src = i == b.nsrc;
+        if (new_src) b.src[b.nsrc++] = st;
+        if (b.per_frame) {
+            // render now, on the caller's stream: the root straight into the frame at its image rows
+            // (RGBA8), a peer into its slot of the send slab -- after that slab's previous exchange
+            // (once per stream and batch)
+            if (b.in_place) {
+                L.k.flags &= ~kFlagSlabRgb24;
+                L.k.out_image_rows = 1u;
+                L.k.cam[0].out = static_cast<uint32_t*>(d_full);
+                if ((r = issue_launch(c, L, nullptr, nullptr, st)) != RRTE_OK) return r;
+            } else {
+                if (new_src) HIPCHK(c, hipStreamWaitEvent(st, c->ev_batch[k], 0));
+                uint8_t* dst = c->d_bsend[k] + (size_t)b.n * b.slice;
+                if ((r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, st)) != RRTE_OK) return r;
+            }
+            b.rendered = b.n + 1;
+        }
         ++b.n;
         hs.lap(3);
         if (b.n == b.cap && (r = flush_batch(c)) != RRTE_OK) return r;
