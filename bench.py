@@ -448,14 +448,45 @@ def main():
             ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), pout(hbuf)))
         reused_ms = (time.perf_counter() - a) / nb * 1e3
         a = time.perf_counter()
+        alloc_s = 0.0
         for _ in range(nb):
+            a0 = time.perf_counter()
             fresh = np.zeros(W * H * 4, dtype=np.uint8)
+            alloc_s += time.perf_counter() - a0
             ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), pout(fresh)))
         fresh_ms = (time.perf_counter() - a) / nb * 1e3
+        # where a fresh buffer's time goes: the allocation (np.zeros: lazily zeroed pages), and the same
+        # call into a fresh buffer whose pages were touched first (the copy no longer takes the page
+        # faults of a never-touched buffer)
+        touched_s = 0.0
+        for _ in range(nb):
+            fresh = np.zeros(W * H * 4, dtype=np.uint8)
+            fresh[::4096] = 1  # first touch of every page, outside the timed call
+            a0 = time.perf_counter()
+            ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), pout(fresh)))
+            touched_s += time.perf_counter() - a0
+        # a pinned buffer (registered once with rrte_hip_host_register, as an engine reusing its frame
+        # buffer would; or page-locked by the caller): the kernel writes the frame into it directly
+        reg = np.zeros(W * H * 4, dtype=np.uint8)
+        ctx.check(lib.rrte_hip_host_register(ctx.h, reg.ctypes.data, reg.nbytes))
+        for _ in range(3):
+            ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), pout(reg)))
+        a = time.perf_counter()
+        for _ in range(nb):
+            ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), pout(reg)))
+        reg_ms = (time.perf_counter() - a) / nb * 1e3
+        reg_ok = bool(np.array_equal(reg, hbuf))
+        ctx.check(lib.rrte_hip_host_unregister(ctx.h, reg.ctypes.data))
         boundary = {"entry": "rrte_hip_render (blocking; Raytracer::render's signature, host RGBA8 out, D2H included)",
                     "ms_per_frame_reused_buffer": round(reused_ms, 4),
                     "ms_per_frame_fresh_buffer": round(fresh_ms, 4),
-                    "frames": nb, "note": "fresh = a new zeroed W*H*4 buffer per frame, as raytracer.rs:54 allocates"}
+                    "fresh_alloc_ms": round(alloc_s / nb * 1e3, 4),
+                    "ms_per_frame_fresh_pretouched": round(touched_s / nb * 1e3, 4),
+                    "ms_per_frame_registered_buffer": round(reg_ms, 4),
+                    "registered_equals_copy_path": reg_ok,
+                    "frames": nb, "note": "fresh = a new zeroed W*H*4 buffer per frame, as raytracer.rs:54 allocates; "
+                                          "registered = the reused buffer pinned once (rrte_hip_host_register): the "
+                                          "kernel stores the frame into it directly, no D2H copy"}
 
     kinds = None
     if world == 1 and not args.no_stock:

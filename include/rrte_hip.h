@@ -279,7 +279,9 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out);
 void rrte_hip_destroy(rrte_ctx* ctx);
 const char* rrte_hip_last_error(const rrte_ctx* ctx);
 
-/* Raytracer::render: blocking; writes W*H*4 bytes to host `out_rgba8`. */
+/* Raytracer::render: blocking; writes W*H*4 bytes to host `out_rgba8`.  When `out_rgba8` is pinned
+ * host memory (hipHostMalloc'd, or a range registered with rrte_hip_host_register) the kernel stores
+ * the frame straight into it while it renders; pageable memory gets one D2H copy after the render. */
 rrte_status rrte_hip_render(rrte_ctx* ctx, const rrte_scene_ir* scene,
                             const rrte_render_params* params, uint8_t* out_rgba8);
 
@@ -416,6 +418,11 @@ rrte_status rrte_hip_flush(rrte_ctx* ctx);
  * (rrte_hip_synchronize, a scene change) renders the open batch but never issues a collective, so
  * neither count may move on one rank alone. */
 rrte_status rrte_hip_gather_info(rrte_ctx* ctx, uint64_t* collectives, uint32_t* open_frames);
+/* Pin a host range the caller keeps alive (e.g. the frame buffer an engine reuses every frame) so
+ * rrte_hip_render writes into it directly.  Unregister (or destroy the context) before freeing it;
+ * rrte_hip_host_unregister waits for the context's frames first. */
+rrte_status rrte_hip_host_register(rrte_ctx* ctx, void* host, size_t bytes);
+rrte_status rrte_hip_host_unregister(rrte_ctx* ctx, void* host);
 
 /* Host-side helpers exported for the bindings (no device work). */
 /* Rows owned by `rank` under the plain band interleave (band b on rank b % nranks). */

@@ -141,6 +141,8 @@ EXPORTS = {
     "rrte_hip_set_gather_batch": (C.c_int, [_P, C.c_uint32]),
     "rrte_hip_flush": (C.c_int, [_P]),
     "rrte_hip_gather_info": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+    "rrte_hip_host_register": (C.c_int, [_P, C.c_void_p, C.c_size_t]),
+    "rrte_hip_host_unregister": (C.c_int, [_P, C.c_void_p]),
     "rrte_hip_set_comm_timeout": (C.c_int, [_P, C.c_uint32]),
 }
 

@@ -218,6 +218,13 @@ struct rrte_ctx {
     // in place, a peer into its slot of the send slab) and only the exchange is batched; RRTE_BATCH_LAUNCH=1
     // keeps round 4's multi-frame launches at the batch's close (A/B)
     bool env_batch_launch = false;
+    // Blocking drop-in path into PINNED host memory (hipHostMalloc'd by the caller, or registered with
+    // rrte_hip_host_register): the kernel stores the frame straight into the caller's buffer over PCIe
+    // while it renders, instead of a render followed by one 8.3 MB D2H copy.  RRTE_BND_ZEROCOPY=0 turns
+    // it off (A/B).  Pageable buffers keep the copy.
+    bool env_bnd_zerocopy = true;
+    struct HostReg { void* p; size_t bytes; };
+    std::vector<HostReg> host_regs;   // rrte_hip_host_register'ed ranges (unregistered at destroy)
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, valid; JitKernel* k; } jit_last{};
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
     // topology kernels (jit.hip JitTopo): the cached scene's topology key and structural decisions, and
@@ -1703,6 +1710,26 @@ rrte_status render_chunked(rrte_ctx* c, const rrte_scene_ir* s, const rrte_rende
     return RRTE_OK;
 }
 
+// The device address of pinned host memory [host, host + bytes) -- hipHostMalloc'd, or registered
+// (rrte_hip_host_register, hipHostRegister) -- or nullptr for pageable memory.  The whole range must
+// lie in one pinned allocation.
+uint32_t* pinned_device_ptr(void* host, size_t bytes) {
+    hipPointerAttribute_t a{}, b{};
+    if (hipPointerGetAttributes(&a, host) != hipSuccess) {
+        (void)hipGetLastError();  // (pageable memory: not an error of this call)
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+    uint8_t* last = static_cast<uint8_t*>(host) + bytes - 1;
+    if (hipPointerGetAttributes(&b, last) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (b.type != hipMemoryTypeHost || static_cast<uint8_t*>(b.devicePointer) != static_cast<uint8_t*>(a.devicePointer) + bytes - 1)
+        return nullptr;
+    return static_cast<uint32_t*>(a.devicePointer);
+}
+
 rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out8,
                           float* outf) {
     rrte_status r = validate(c, s, p);
@@ -1717,12 +1744,14 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     const int nr = c->nranks, rk = c->rank;
     c->nranks = 1;
     c->rank = 0;
-    const bool chunked = out8 && !outf && c->bnd_chunks > 1 && p->height >= 32u && !c->env_debug;
+    // pinned caller buffer: the kernel writes the frame into it directly (no D2H copy afterwards)
+    uint32_t* zc = out8 && !outf && c->env_bnd_zerocopy ? pinned_device_ptr(out8, npix * 4) : nullptr;
+    const bool chunked = !zc && out8 && !outf && c->bnd_chunks > 1 && p->height >= 32u && !c->env_debug;
     if (chunked) {
         r = render_chunked(c, s, p, out8, (uint32_t)c->bnd_chunks);
     } else {
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        r = launch(c, s, p, p->height, c->d_rgba, outf ? c->d_f32 : nullptr, c->stream);
+        r = launch(c, s, p, p->height, zc ? zc : c->d_rgba, outf ? c->d_f32 : nullptr, c->stream);
         if (r == RRTE_OK) r = hipEventRecord(c->ev1, c->stream) == hipSuccess ? RRTE_OK : RRTE_HIP_ERROR;
     }
     c->nranks = nr;
@@ -1732,7 +1761,7 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     c->pending_primary = (uint64_t)npix * p->samples_per_pixel;
     c->stats.upload_ms = up;
     c->stats.gather_ms = 0.0;
-    if (out8 && !chunked) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
+    if (out8 && !chunked && !zc) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
     if (outf) HIPCHK(c, hipMemcpyAsync(outf, c->d_f32, npix * 16, hipMemcpyDeviceToHost, c->stream));
     if ((r = finish_frame(c)) != RRTE_OK) return r;
     c->stats.frames++;
@@ -1810,6 +1839,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_PRIO_SLOTS")) c->env_prio_slots = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
     if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] == '1';
+    if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
     if (const char* g = getenv("RRTE_NOCOMM_WAIT_MS")) c->env_nocomm_wait_ms = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
@@ -1870,6 +1900,7 @@ void rrte_hip_destroy(rrte_ctx* c) {
     if (c->comm && wait_bounded(c) != RRTE_OK) c->comm = nullptr;  // (comm_abort has aborted it)
     (void)hipDeviceSynchronize();
     if (c->comm) ncclCommDestroy(c->comm);
+    for (const auto& hr : c->host_regs) (void)hipHostUnregister(hr.p);
     c->jit_pending.clear();  // joins background compiles
     for (auto& kv : c->jit_cache) jit_release(kv.second);
     for (auto& B : c->sb) {
@@ -2732,6 +2763,30 @@ rrte_status rrte_hip_set_gather_batch(rrte_ctx* c, uint32_t frames) {
 rrte_status rrte_hip_flush(rrte_ctx* c) {
     if (!c) return RRTE_INVALID_ARG;
     return flush_batch(c);
+}
+
+rrte_status rrte_hip_host_register(rrte_ctx* c, void* host, size_t bytes) {
+    if (!c || !host || bytes == 0) return fail(c, RRTE_INVALID_ARG, "null or empty host range");
+    HIPCHK(c, hipSetDevice(c->device));
+    unsigned flags = hipHostRegisterMapped;
+    if (const char* g = getenv("RRTE_HOST_REGISTER_FLAGS")) flags = (unsigned)strtoul(g, nullptr, 0);  // (A/B)
+    HIPCHK(c, hipHostRegister(host, bytes, flags));
+    c->host_regs.push_back({host, bytes});
+    return RRTE_OK;
+}
+
+rrte_status rrte_hip_host_unregister(rrte_ctx* c, void* host) {
+    if (!c || !host) return RRTE_INVALID_ARG;
+    for (size_t i = 0; i < c->host_regs.size(); ++i)
+        if (c->host_regs[i].p == host) {
+            HIPCHK(c, hipSetDevice(c->device));
+            rrte_status r = rrte_hip_synchronize(c);  // (no frame may still write into it)
+            if (r != RRTE_OK) return r;
+            HIPCHK(c, hipHostUnregister(host));
+            c->host_regs.erase(c->host_regs.begin() + (long)i);
+            return RRTE_OK;
+        }
+    return fail(c, RRTE_INVALID_ARG, "host range %p was not registered with this context", host);
 }
 
 rrte_status rrte_hip_gather_info(rrte_ctx* c, uint64_t* collectives, uint32_t* open_frames) {

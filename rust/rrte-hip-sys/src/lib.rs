@@ -144,6 +144,8 @@ extern "C" {
     pub fn rrte_hip_set_gather_batch(ctx: *mut rrte_ctx, frames: u32) -> rrte_status;
     pub fn rrte_hip_flush(ctx: *mut rrte_ctx) -> rrte_status;
     pub fn rrte_hip_gather_info(ctx: *mut rrte_ctx, collectives: *mut u64, open_frames: *mut u32) -> rrte_status;
+    pub fn rrte_hip_host_register(ctx: *mut rrte_ctx, host: *mut c_void, bytes: usize) -> rrte_status;
+    pub fn rrte_hip_host_unregister(ctx: *mut rrte_ctx, host: *mut c_void) -> rrte_status;
     pub fn rrte_hip_band_rows_for_rank(height: u32, band_rows: u32, nranks: c_int, rank: c_int) -> u32;
     pub fn rrte_hip_band_layout(scene: *const rrte_scene_ir, params: *const rrte_render_params, nranks: c_int,
                                 root: c_int, sky_bands: *mut u32, root_bands: *mut u32,

@@ -87,3 +87,34 @@ def test_chunked_blocking_render_is_exact(chunks, w, h, monkeypatch):
         assert np.array_equal(got, want), f"frame {f}: {int((got != want).sum())} bytes differ"
         assert int(ctx.stats().shadow_rays) == want_shadow
     ctx.close()
+
+
+@pytest.mark.parametrize("name,w,h", [("sdf-showcase", 1920, 1080), ("sdf-showcase", 333, 97),
+                                      ("mesh-demo", 200, 120)])
+def test_pinned_buffers_are_written_directly(name, w, h):
+    """A registered buffer (rrte_hip_host_register, pinned once) and a caller-pinned buffer (torch
+    pin_memory: hipHostMalloc) take the zero-copy route -- the kernel stores the frame into host memory
+    -- and must hold exactly the copy path's bytes, frame after frame; unregistering is checked."""
+    import torch
+    objs, lights, cam, cfg = scenes.SCENES[name](w, h)
+    sc = LoweredScene(objs, lights, cam)
+    prm = cfg.lower()
+    ctx = Context(0, jit=abi.JIT_ON)
+    want = _blocking(ctx, sc, prm, np.zeros(w * h * 4, np.uint8)).copy()
+    reg = np.full(w * h * 4 + 64, 7, np.uint8)[16:16 + w * h * 4]  # (not page aligned)
+    ctx.check(ctx.lib.rrte_hip_host_register(ctx.h, reg.ctypes.data, reg.nbytes))
+    for f in range(3):
+        reg[:] = 7
+        got = _blocking(ctx, sc, prm, reg)
+        assert np.array_equal(got, want), f"registered, frame {f}: {int((got != want).sum())} bytes differ"
+    ctx.check(ctx.lib.rrte_hip_host_unregister(ctx.h, reg.ctypes.data))
+    assert ctx.lib.rrte_hip_host_unregister(ctx.h, reg.ctypes.data) == abi.RRTE_INVALID_ARG
+    reg[:] = 7
+    assert np.array_equal(_blocking(ctx, sc, prm, reg), want)  # pageable again: the copy path
+    pinned = torch.full((w * h * 4,), 7, dtype=torch.uint8).pin_memory()
+    for f in range(2):
+        ctx.check(ctx.lib.rrte_hip_render(ctx.h, sc.ref(), C.byref(prm),
+                                          C.cast(pinned.data_ptr(), C.POINTER(C.c_uint8))))
+        got = pinned.numpy()
+        assert np.array_equal(got, want), f"pinned, frame {f}: {int((got != want).sum())} bytes differ"
+    ctx.close()
