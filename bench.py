@@ -165,18 +165,27 @@ def flop_tally(scene, params):
     return flops, int(cnt.sdf_steps), int(cnt.samples + cnt.shadow_rays)
 
 
-def pmc_traffic(workload_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_*.json), or None."""
-    best = None
+def pmc_traffic(workload_key, build_id):
+    """The committed rocprofv3 PMC summary (profiles/pmc_*.json) of this workload AND this build
+    (rrte_hip_build_id: device headers + hiprtc options), or None; plus a note naming the newest
+    summary of the workload when none matches the build (its counters are then not reported)."""
+    best, newest = None, None
     for p in sorted((ROOT / "profiles").glob("pmc_*.json")):
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
-        if d.get("workload") == workload_key and d.get("hbm_bytes_per_launch") is not None:
-            if best is None or d.get("created", 0) >= best.get("created", 0):
-                best = d
-    return best
+        if d.get("workload") != workload_key or d.get("hbm_bytes_per_launch") is None:
+            continue
+        d["file"] = f"profiles/{p.name}"
+        if newest is None or d.get("created", 0) >= newest.get("created", 0):
+            newest = d
+        if d.get("build_id") == build_id and (best is None or d.get("created", 0) >= best.get("created", 0)):
+            best = d
+    note = {"build_id": build_id, "profile": best["file"] if best else None, "build_id_match": best is not None}
+    if best is None and newest is not None:
+        note["newest_profile_of_another_build"] = newest["file"]
+    return best, note
 
 
 def measured_valu_peak():
@@ -529,7 +538,7 @@ def main():
         flops_launch = flops_frame * rows / H
         valu_tf = flops_launch / (avg_launch_ms * 1e-3) / 1e12
         wl = f"{args.scene}@{W}x{H}/{args.mode}"
-        pmc = pmc_traffic(wl)
+        pmc, pmc_note = pmc_traffic(wl, abi.build_id())
         line = {
             "metric": "Mray/s (primary+shadow) at 1920x1080, sdf-showcase scene; 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -566,7 +575,8 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": valu_tf / VALU_PEAK_TFLOPS,
                 "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/pmc_*.json)",
+                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/pmc_*.json of this build)",
+                "profile": pmc_note,
                 "flops_per_launch": flops_launch,
                 "frac_of_unpacked_peak": valu_tf / (VALU_PEAK_TFLOPS / 2),
                 "achieved_at_frame_rate": round(flops_launch / (elapsed / args.steps) / 1e12, 3),

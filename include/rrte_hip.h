@@ -359,6 +359,10 @@ rrte_status rrte_hip_sdf_guards(const rrte_sdf_node* in, uint32_t count, uint32_
  * (y << 16 | x) to slots[0..cap); RRTE_INVALID_ARG if they do not fit. */
 rrte_status rrte_hip_tile_order_plan(const uint32_t* costs, uint32_t tiles, uint32_t tiles_x, uint32_t* slots,
                                      uint32_t cap, uint32_t* n_slots);
+/* Diagnostic: the build id of the device code (32 hex digits): a hash of the embedded device headers,
+ * every hiprtc option (RRTE_JIT_EXTRA_OPTS included) and the hiprtc version.  Profiles record it
+ * (tools/prof.sh) and bench.py takes counters only from a profile of the same build. */
+rrte_status rrte_hip_build_id(char* out, size_t out_len);
 /* Diagnostic (host only): the persistent JIT cache's file name (32 hex digits + NUL, out_len >= 33)
  * for a generated kernel `source`: a hash of the source, the device headers embedded in this library
  * (or `headers_override` in their place, to show that a rebuilt library's headers change the key),

@@ -141,6 +141,7 @@ EXPORTS = {
     "rrte_hip_set_gather_batch": (C.c_int, [_P, C.c_uint32]),
     "rrte_hip_flush": (C.c_int, [_P]),
     "rrte_hip_gather_info": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+    "rrte_hip_build_id": (C.c_int, [C.c_char_p, C.c_size_t]),
     "rrte_hip_host_register": (C.c_int, [_P, C.c_void_p, C.c_size_t]),
     "rrte_hip_host_unregister": (C.c_int, [_P, C.c_void_p]),
     "rrte_hip_set_comm_timeout": (C.c_int, [_P, C.c_uint32]),
@@ -190,3 +191,12 @@ def band_layout(scene_ref, params_ref, nranks: int, root: int = 0) -> tuple:
     if st != RRTE_OK:
         raise RuntimeError(f"rrte_hip_band_layout: status {st}")
     return sky.value, rb.value, pb.value
+
+
+def build_id() -> str:
+    """rrte_hip_build_id: the device code's identity (headers, hiprtc options, hiprtc version)."""
+    buf = C.create_string_buffer(64)
+    st = load().rrte_hip_build_id(buf, 64)
+    if st != RRTE_OK:
+        raise RuntimeError(f"rrte_hip_build_id: status {st}")
+    return buf.value.decode()

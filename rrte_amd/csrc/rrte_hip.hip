@@ -2082,6 +2082,14 @@ rrte_status rrte_hip_tile_order_plan(const uint32_t* costs, uint32_t tiles, uint
     return RRTE_OK;
 }
 
+rrte_status rrte_hip_build_id(char* out, size_t out_len) {
+    if (!out || out_len < 33) return RRTE_INVALID_ARG;
+    // the device code's identity: the embedded headers, every hiprtc option (RRTE_JIT_EXTRA_OPTS
+    // included) and the hiprtc version -- the JIT cache key of an empty source
+    snprintf(out, out_len, "%s", jit_cache_name(std::string(), nullptr).c_str());
+    return RRTE_OK;
+}
+
 rrte_status rrte_hip_jit_cache_key(const char* source, const char* headers_override, char* out, size_t out_len) {
     if (!source || !out || out_len < 33) return RRTE_INVALID_ARG;
     snprintf(out, out_len, "%s", jit_cache_name(source, headers_override).c_str());

@@ -144,6 +144,7 @@ extern "C" {
     pub fn rrte_hip_set_gather_batch(ctx: *mut rrte_ctx, frames: u32) -> rrte_status;
     pub fn rrte_hip_flush(ctx: *mut rrte_ctx) -> rrte_status;
     pub fn rrte_hip_gather_info(ctx: *mut rrte_ctx, collectives: *mut u64, open_frames: *mut u32) -> rrte_status;
+    pub fn rrte_hip_build_id(out: *mut c_char, out_len: usize) -> rrte_status;
     pub fn rrte_hip_host_register(ctx: *mut rrte_ctx, host: *mut c_void, bytes: usize) -> rrte_status;
     pub fn rrte_hip_host_unregister(ctx: *mut rrte_ctx, host: *mut c_void) -> rrte_status;
     pub fn rrte_hip_band_rows_for_rank(height: u32, band_rows: u32, nranks: c_int, rank: c_int) -> u32;

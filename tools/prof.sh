@@ -12,6 +12,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export GPU_MAX_HW_QUEUES=32
+( cd $R && python3 -c "from rrte_amd import abi; print(abi.build_id())" ) > $OUT/build_id.txt || exit 1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $R/bench.py --no-cpu --no-stock --inflight 1 --steps 20 > $OUT/trace.log 2>&1 || { tail $OUT/trace.log; exit 1; }
 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/tl -o run -- python3 $R/bench.py --no-cpu --no-stock --steps 20 --warmup 5 > $OUT/tl.log 2>&1 || { tail $OUT/tl.log; exit 1; }

@@ -35,7 +35,8 @@ if stats.exists():
     for r in csv.DictReader(open(stats)):
         if KERNEL_RE.search(r["Name"]):
             dur_ns = float(r["AverageNs"])
-res = {"created": time.time(), "workload": workload, "kernel": meta.get("Kernel_Name"), "dispatch": meta, "counters_per_dispatch": avg,
+bid = src / "build_id.txt"  # (tools/prof.sh: rrte_hip_build_id of the profiled build)
+res = {"created": time.time(), "workload": workload, "build_id": bid.read_text().strip() if bid.exists() else None, "kernel": meta.get("Kernel_Name"), "dispatch": meta, "counters_per_dispatch": avg,
        "avg_kernel_ns": dur_ns}
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     fetch = avg["FETCH_SIZE"] * 1024 * 2  # gfx950: FETCH_SIZE reads 1/2 of wide coalesced reads
