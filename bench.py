@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=4,
                     help="N > 1: caller streams the frames rotate over (each frame is launched at its call on its "
                          "stream; frames in flight), independent of the gather batch (--inflight)")
+    ap.add_argument("--flyby", type=int, default=0,
+                    help="camera fly-by: frame i renders camera pose i %% K of K poses orbiting the scene's target "
+                         "(0.6 degrees apart; pose 0 = the scene's own camera); 0 = static camera")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
@@ -141,18 +144,20 @@ def oracle_frame(scene, params):
     return out8, shadow
 
 
-def verify_frames(frames_u8, timed_shadow, steps, ref):
+def verify_frames(frames_u8, timed_shadow, steps, ref, refs=None, shadow_total=None):
     """The timed frames against the oracle: every buffer in flight holds the last
     timed frame rendered into it; compared byte for byte with the oracle's RGBA8 frame of the same
     scene and parameters (the device gamma byte is proven identical to its powf path; glibc's powf
     may differ by an ulp, hence u8 max diff <= 1 as the bar), and the timed frames' shadow-ray total
     with steps x the oracle's count (exact)."""
-    ref8, ref_shadow = ref
-    diffs = [np.abs(f.astype(np.int16) - ref8.astype(np.int16)) for f in frames_u8]
+    if refs is None:
+        refs = [ref] * len(frames_u8)
+        shadow_total = steps * int(ref[1])
+    diffs = [np.abs(f.astype(np.int16) - r8.astype(np.int16)) for f, (r8, _) in zip(frames_u8, refs)]
     return {"frames": len(frames_u8), "u8_max_diff": int(max(int(d.max()) for d in diffs)),
             "bytes_differing": int(sum(int((d != 0).sum()) for d in diffs)),
-            "shadow_rays_match": int(timed_shadow) == steps * int(ref_shadow),
-            "shadow_rays_per_frame": {"timed_mean": timed_shadow / steps, "oracle": int(ref_shadow)},
+            "shadow_rays_match": int(timed_shadow) == int(shadow_total),
+            "shadow_rays_per_frame": {"timed_mean": timed_shadow / steps, "oracle": shadow_total / steps},
             "reference": "oracle/rrte_oracle.c (C restatement of Raytracer::render), same scene and parameters"}
 
 
@@ -299,6 +304,19 @@ def main():
         cfg.jitter = "random"
     scene = LoweredScene(objs, lights, cam)
     prm = cfg.lower()
+    poses = [scene]
+    if args.flyby > 1:  # an orbit about the target the examples aim at (rrte_amd.scenes: look_at (0, 2, 0))
+        import copy
+        import math
+        from rrte_amd.math import vec3
+        p0 = [float(v) for v in cam.transform.position]
+        for k in range(1, args.flyby):
+            c2 = copy.deepcopy(cam)
+            a = 0.0105 * k
+            dx, dz = p0[0], p0[2]
+            c2.transform.position = vec3(dx * math.cos(a) - dz * math.sin(a), p0[1], dx * math.sin(a) + dz * math.cos(a))
+            c2.look_at((0.0, 2.0, 0.0))
+            poses.append(LoweredScene(objs, lights, c2))
     # N > 1: every frame is launched at its call on one of --streams caller streams (frames in flight)
     # -- rank 0 writing its own bands straight into the frame buffers, the peers into their send slabs
     # -- and the frames are exchanged in batches of F (rrte_hip_set_gather_batch): ONE grouped
@@ -332,6 +350,8 @@ def main():
 
     # the call arguments are built once: the loop below is the library's host path plus one ctypes call
     h, sref, pref = ctx.h, scene.ref(), C.byref(prm)
+    srefs = [ps.ref() for ps in poses]
+    K = len(srefs)
     fptrs = [f.data_ptr() for f in fulls]
     render_gather, render_async = lib.rrte_hip_render_gather_async, lib.rrte_hip_render_async
 
@@ -339,9 +359,9 @@ def main():
         j = i % F
         if gath:
             # each frame launched at its call on caller stream i % NS; the exchange is batched
-            st = render_gather(h, sref, pref, 0, fptrs[j] if rank == 0 else None, sptrs[i % NS])
+            st = render_gather(h, srefs[i % K], pref, 0, fptrs[j] if rank == 0 else None, sptrs[i % NS])
         else:
-            st = render_async(h, sref, pref, fptrs[j], None, sptrs[j])
+            st = render_async(h, srefs[i % K], pref, fptrs[j], None, sptrs[j])
         if st:
             ctx.check(st)
 
@@ -640,7 +660,15 @@ def main():
                 line["stock_config"]["gpu_over_cpu"] = round(stock["value"] / line["cpu_baseline"]["stock_config"]["value"], 2)
         else:
             ref = oracle_frame(scene, prm)
-        line["verified"] = verify_frames(timed_frames, shadow, args.steps, ref)  # (shadow: summed over ranks)
+        if K > 1:  # fly-by: every buffer against the oracle frame of its last frame's pose
+            refs = [oracle_frame(ps, prm) for ps in poses]
+            last = [max(i for i in range(args.steps) if i % F == j) for j in range(len(timed_frames))]
+            line["verified"] = verify_frames(timed_frames, shadow, args.steps, None,
+                                             refs=[refs[i % K] for i in last],
+                                             shadow_total=sum(refs[i % K][1] for i in range(args.steps)))
+            line["config"]["flyby_poses"] = K
+        else:
+            line["verified"] = verify_frames(timed_frames, shadow, args.steps, ref)  # (shadow: summed over ranks)
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist_on:
