@@ -91,6 +91,20 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def physical_cores():
+    """Physical cores of the host (distinct (physical id, core id) pairs in /proc/cpuinfo), or None."""
+    try:
+        cores, phys = set(), "0"
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":", 1)[1].strip()))
+        return len(cores) or None
+    except OSError:
+        return None
+
+
 def cpu_baseline(scene, params, budget_s, stock=None):
     """The oracle (C restatement of Raytracer::render) on this host's cores (SURVEY §8d):
     N threads: median of up to 5 whole frames after 1 warm-up; 1 thread: one whole frame (or a
@@ -125,6 +139,16 @@ def cpu_baseline(scene, params, budget_s, stock=None):
     t1 = time.perf_counter() - t0
     out["single_thread"] = {"value": (W * (rows[1] - rows[0]) * params.samples_per_pixel + sh1) / t1 / 1e6,
                             "unit": "Mray/s", "cores": 1, "rows": list(rows)}
+    # the whole host, extrapolated: the job may use `threads` of the host's CPUs
+    # (its affinity share); the measured per-thread rate at that thread count x the host's physical
+    # cores is an upper estimate of the reference's rayon path on the whole machine (no SMT gain)
+    phys = physical_cores()
+    if phys:
+        per_thread = out["value"] / threads
+        out["whole_host_extrapolation"] = {
+            "value": round(per_thread * phys, 1), "unit": "Mray/s", "physical_cores": phys,
+            "note": f"{per_thread:.2f} Mray/s per thread at {threads} threads x {phys} physical cores "
+                    "(linear scaling assumed: an upper estimate, not a measurement)"}
     if stock is not None:  # reference stock config (spp 4, depth 50, random jitter/scatter) on a row band
         sscene, sprm, band = stock
         t0 = time.perf_counter()
@@ -656,6 +680,9 @@ def main():
             line["cpu_baseline"], ref = cpu_baseline(scene, prm, args.cpu_seconds,
                                                      stock=(*stock_config(args), sband) if stock else None)
             line["cpu_baseline"]["gpu_over_cpu"] = round(value / line["cpu_baseline"]["value"], 2)
+            if "whole_host_extrapolation" in line["cpu_baseline"]:
+                wh = line["cpu_baseline"]["whole_host_extrapolation"]
+                wh["gpu_over_whole_host"] = round(value / wh["value"], 2)
             if stock and "stock_config" in line["cpu_baseline"]:
                 line["stock_config"]["gpu_over_cpu"] = round(stock["value"] / line["cpu_baseline"]["stock_config"]["value"], 2)
         else:

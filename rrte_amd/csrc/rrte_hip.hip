@@ -272,8 +272,11 @@ struct rrte_ctx {
         uint32_t* d_list[kVersions] = {};
         size_t cap_list[kVersions] = {};  // words
         Retire ret[kVersions];
-        uint32_t* h_list = nullptr;      // pinned staging
+        hipEvent_t ev_up[kVersions] = {};                 // the version's upload copy done
+        std::vector<hipStream_t> ordered[kVersions];     // streams already made to wait for ev_up
+        uint32_t* h_list = nullptr;      // pinned staging (reused once the last upload's copy is done)
         size_t cap_h_list = 0;
+        hipEvent_t ev_stage = nullptr;   // the last upload's copy out of h_list done
         hipStream_t upload_stream = nullptr;
         int cur = -1;                    // version holding `slots` (-1: not uploaded)
         uint64_t launches = 0;           // launches of `key` since its last profile
@@ -1425,7 +1428,9 @@ std::vector<uint32_t> fixed_slots(uint32_t n, uint32_t tiles_x) {
 // call) allocates nothing.
 bool reserve_hot_lists(rrte_ctx::TileProfile& tp, size_t words) {
     if (tp.cap_h_list < words) {
-        if (tp.h_list) (void)hipHostFree(tp.h_list);  // (pinned staging: every copy from it was synchronised)
+        // (pinned staging: the last copy out of it must be done -- the upload stream holds copies only)
+        if (tp.ev_stage && hipEventSynchronize(tp.ev_stage) != hipSuccess) return false;
+        if (tp.h_list) (void)hipHostFree(tp.h_list);
         tp.h_list = nullptr;
         tp.cap_h_list = 0;
         if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), words * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
@@ -1444,10 +1449,12 @@ bool reserve_hot_lists(rrte_ctx::TileProfile& tp, size_t words) {
 // Uploads the composed slots into a free version of the device list; false leaves the launch on the
 // current list (or in image order) -- it never waits for the device.  The current version is retired
 // first; a version is free once every launch that read it has completed (struct Retire).  The copy
-// runs on the list's own upload stream and is synchronised (it holds nothing else), so every launch
-// sees a whole list.
+// runs on the list's own upload stream; its event orders every stream's first launch that reads the
+// version after it (plan_tile_order), so every launch sees a whole list and no render call waits.
 bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
     constexpr int K = rrte_ctx::TileProfile::kVersions;
+    // the staging buffer still feeds the previous upload's copy: keep the current list for now
+    if (tp.ev_stage && hipEventQuery(tp.ev_stage) != hipSuccess) return false;
     int pick = -1;
     for (int k = 1; k <= K && pick < 0; ++k) {  // the oldest retired version first
         const int v = (int)((tp.uploads + (uint64_t)k) % K);
@@ -1466,9 +1473,13 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
     }
     if (!reserve_hot_lists(tp, words)) return false;
     memcpy(tp.h_list, tp.slots.data(), bytes);
+    if (!tp.ev_up[pick] && hipEventCreateWithFlags(&tp.ev_up[pick], hipEventDisableTiming) != hipSuccess) return false;
+    if (!tp.ev_stage && hipEventCreateWithFlags(&tp.ev_stage, hipEventDisableTiming) != hipSuccess) return false;
     if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
-        hipStreamSynchronize(tp.upload_stream) != hipSuccess)
+        hipEventRecord(tp.ev_up[pick], tp.upload_stream) != hipSuccess ||
+        hipEventRecord(tp.ev_stage, tp.upload_stream) != hipSuccess)
         return false;
+    tp.ordered[pick].clear();
     if (tp.cur >= 0 && retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
     tp.cur = pick;
     ++tp.uploads;
@@ -1544,6 +1555,11 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         tp.cur = -1;
     }
     if (!tp.slots.empty() && tp.slots.size() == tiles && (tp.cur >= 0 || upload_hot_list(c, tp))) {
+        auto& ord = tp.ordered[tp.cur];  // (first launch of this stream on the version: after its upload)
+        if (tp.ev_up[tp.cur] && std::find(ord.begin(), ord.end(), st) == ord.end()) {
+            if (hipStreamWaitEvent(st, tp.ev_up[tp.cur], 0) != hipSuccess) return false;
+            ord.push_back(st);
+        }
         k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
         k.prio_slots = std::min(c->env_prio_slots, k.hot_n);
@@ -1929,6 +1945,9 @@ void rrte_hip_destroy(rrte_ctx* c) {
             destroy_events(tp.ret[i]);
         }
         if (tp.h_list) (void)hipHostFree(tp.h_list);
+        for (hipEvent_t e : tp.ev_up)
+            if (e) (void)hipEventDestroy(e);
+        if (tp.ev_stage) (void)hipEventDestroy(tp.ev_stage);
         if (tp.upload_stream) (void)hipStreamDestroy(tp.upload_stream);
     }
     for (int i = 0; i < rrte_ctx::kBndChunksMax; ++i) {
