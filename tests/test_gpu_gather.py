@@ -52,6 +52,17 @@ def test_gather_path_matches_plain_render(overlap, jit, batch, route, monkeypatc
     _check_gather(overlap, jit, batch, monkeypatch, None)
 
 
+@pytest.mark.parametrize("route", ["in_place", "self"])
+@pytest.mark.parametrize("batch", [3, 8])
+def test_multi_frame_batch_launches(batch, route, monkeypatch):
+    """RRTE_BATCH_LAUNCH=1: a batch's frames rendered together in multi-frame launches at its close
+    (round 4's policy, kept as an A/B switch) instead of one launch per frame at its call."""
+    monkeypatch.setenv("RRTE_BATCH_LAUNCH", "1")
+    if route == "self":
+        monkeypatch.setenv("RRTE_GATHER_SELF", "1")
+    _check_gather(False, abi.JIT_ON, batch, monkeypatch, None)
+
+
 @pytest.mark.parametrize("alpha,rgb24", [(None, "0"), ("material", "1"), ("spp2", "1")])
 def test_gather_slab_formats(alpha, rgb24, monkeypatch):
     """RGBA8 slabs when forced (RRTE_GATHER_RGB24=0) or when some alpha byte is not 255; every

@@ -1,0 +1,70 @@
+"""Kernel variants behind build switches, each held to the parity bar against the oracle (linear image
+bit-exact, shadow-ray counts exact): the shadow-ray repacking of the scene-specialised kernel
+(RRTE_SHADOW_REPACK), the branch-free correctly rounded square root (RRTE_SQRT_BRANCHFREE; its
+exhaustive proof is tests/test_gpu_fpexact.py), and the generic kernel's all-features build next to
+the per-scene feature variants the host picks (RRTE_GENERIC_ALL)."""
+import numpy as np
+import pytest
+
+import scenes_extra as se
+from rrte_amd import AmbientLight, Raytracer, scenes
+from rrte_amd import abi
+from test_gpu_parity import compare
+
+pytestmark = pytest.mark.gpu
+
+
+def _ambient_showcase(w, h, mode="lambert_shadow"):
+    """sdf-showcase with an ambient light between its point lights (the repacked shading adds every
+    light's term in light order, ambient included)."""
+    objs, lights, cam, cfg = scenes.sdf_showcase(w, h, mode=mode)
+    lights.insert(1, AmbientLight.default_ambient())
+    return objs, lights, cam, cfg
+
+
+CASES = {
+    "sdf-showcase": lambda: scenes.sdf_showcase(320, 180),
+    "sdf-showcase-1080p": lambda: scenes.sdf_showcase(1920, 1080),
+    "advanced-demo": lambda: scenes.advanced_demo(320, 180),      # 5 point lights: up to 5 rounds
+    "basic-demo": lambda: scenes.basic_demo(320, 240, mode="lambert_shadow"),
+    "ambient": lambda: _ambient_showcase(320, 180),
+    "deformers": lambda: se.deformers_scene(200, 120, "lambert_shadow"),
+    "cull-stress": lambda: se.cull_stress_scene(240, 160, "lambert_shadow", n_spheres=40),
+    "all-lights": lambda: se.all_lights_scene(200, 120, "lambert_shadow"),  # (not repacked: spot, directional)
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+@pytest.mark.parametrize("opt", ["-DRRTE_SHADOW_REPACK=1", "-DRRTE_SQRT_BRANCHFREE"])
+def test_specialised_kernel_variant_matches_oracle(case, opt, monkeypatch):
+    monkeypatch.setenv("RRTE_JIT_EXTRA_OPTS", opt)
+    compare(*CASES[case](), linear_exact=case != "all-lights", jit=abi.JIT_ON)
+
+
+@pytest.mark.parametrize("case", ["sdf-showcase", "advanced-demo", "ambient"])
+def test_shadow_repack_equals_plain_loop(case, monkeypatch):
+    """Bit for bit against the plain shading loop on the same specialised kernel path, culling on and
+    off (the repacked rounds test under the union of their lights' cull masks)."""
+    objs, lights, cam, cfg = CASES[case]()
+    out = {}
+    for cull in ("0", "1"):
+        monkeypatch.setenv("RRTE_CULL", cull)
+        for opt in ("", "-DRRTE_SHADOW_REPACK=1"):
+            monkeypatch.setenv("RRTE_JIT_EXTRA_OPTS", opt)
+            rt = Raytracer(cfg, device=0, jit=abi.JIT_ON)
+            _, lin = rt.render_f32(objs, lights, [], cam, linear=True)
+            out[(cull, opt)] = (lin.view(np.uint32).copy(), int(rt.stats().shadow_rays))
+    ref = out[("1", "")]
+    for k, v in out.items():
+        assert np.array_equal(v[0], ref[0]), k
+        assert v[1] == ref[1], k
+
+
+@pytest.mark.parametrize("name,mode", [("sdf-showcase", "lambert_shadow"), ("basic-demo", "refcompat"),
+                                       ("sdf-showcase-literal", "lambert_shadow"), ("mesh-demo", "lambert_shadow")])
+def test_generic_all_features_build(name, mode, monkeypatch):
+    """The generic kernel with every feature compiled in (RRTE_GENERIC_ALL=1) and the feature
+    variant the host picks for the scene both match the oracle."""
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RRTE_GENERIC_ALL", flag)
+        compare(*scenes.SCENES[name](200, 120, mode=mode), jit=abi.JIT_OFF)
