@@ -401,6 +401,9 @@ __device__ __forceinline__ bool sdf_guard(G& gp, uint32_t gop, const float* gf, 
 // wave-uniform (every lane runs the same program), so the stacks stay in
 // registers indexed by SGPR values.  A guarded operand is skipped when its
 // guard holds for the whole wave.
+#ifndef RRTE_SDF_FASTPATH
+#define RRTE_SDF_FASTPATH 1  // generic kernel: one-leaf / leaf-leaf-op programs off the stack machine (A/B)
+#endif
 template <uint32_t F = kFeatAll>
 struct SdfProgramT {
     static constexpr bool kSmall = false;
@@ -408,6 +411,27 @@ struct SdfProgramT {
     uint32_t count;
     template <class G>
     __device__ __forceinline__ float eval(f3 p, G& g) const {
+        // The two shapes most objects have -- one leaf, or two leaves under one CSG op (no deformer,
+        // no guard: guards need operands of >= 2 leaves) -- evaluate without the stack machine: no
+        // per-node loop, no dynamically indexed stack, and the nodes' scalar loads do not depend on
+        // a loop counter (the march loop around this call can keep them in SGPRs).  Same operations
+        // in the same order as the loop below, so the same bits.
+        const uint32_t op0 = nodes[0].op;
+        if (RRTE_SDF_FASTPATH && count == 1u && op0 < 32u) return sdf_leaf(g, op0, nodes[0].f, p);
+        if (RRTE_SDF_FASTPATH && count == 3u && op0 < 32u && nodes[1].op < 32u && nodes[2].op >= 32u && nodes[2].op < 64u &&
+            nodes[1].i[2] == 0u) {
+            const float a = sdf_leaf(g, op0, nodes[0].f, p);
+            const float b = sdf_leaf(g, nodes[1].op, nodes[1].f, p);
+            const float k = nodes[2].f[0];
+            switch (nodes[2].op) {
+            case RRTE_SDF_UNION: return smn(a, b);
+            case RRTE_SDF_DIFFERENCE: return smx(a, -b);
+            case RRTE_SDF_INTERSECTION: return smx(a, b);
+            case RRTE_SDF_SMOOTH_UNION: return smin(g, a, b, k);
+            case RRTE_SDF_SMOOTH_DIFFERENCE: return -smin(g, -a, b, k);
+            default: return -smin(g, -a, -b, k);
+            }
+        }
         float vs[RRTE_SDF_MAX_STACK];
         f3 ps[(F & kFeatDeform) ? RRTE_SDF_MAX_POINT_STACK : 1];
         uint32_t sp = 0, pp = 0;

@@ -72,6 +72,9 @@ impl SceneIr {
 /// One rrte_hip context on one HIP device.
 pub struct Context {
     ctx: *mut rrte_ctx,
+    // a frame buffer the context owns and keeps pinned (rrte_hip_host_register): rrte_hip_render
+    // writes frames straight into it (no D2H copy after the render)
+    frame: Option<Vec<u8>>,
 }
 
 // A context may move between threads (it is used by one thread at a time: `&mut self`).
@@ -89,7 +92,7 @@ impl Context {
             unsafe { rrte_hip_destroy(ctx) };
             return Err(Error { status: RRTE_INVALID_ARG, message: "librrte_hip ABI version mismatch".into() });
         }
-        Ok(Self { ctx })
+        Ok(Self { ctx, frame: None })
     }
 
     fn check(&self, st: rrte_status) -> Result<(), Error> {
@@ -116,6 +119,52 @@ impl Context {
         let ir = scene.raw();
         let st = unsafe { rrte_hip_render(self.ctx, &ir, params, out.as_mut_ptr()) };
         self.check(st)
+    }
+
+    /// Keeps `buf` (at least W*H*4 bytes of the frames to come) as the context's pinned frame buffer:
+    /// `render_pinned` then has the kernel store each frame straight into it.  A previous buffer is
+    /// unpinned and dropped.
+    pub fn set_frame_buffer(&mut self, mut buf: Vec<u8>) -> Result<(), Error> {
+        drop(self.take_frame_buffer()?);
+        self.check(unsafe { rrte_hip_host_register(self.ctx, buf.as_mut_ptr() as *mut c_void, buf.len()) })?;
+        self.frame = Some(buf);
+        Ok(())
+    }
+
+    /// Unpins the frame buffer (after the context's frames have completed) and hands it back.
+    pub fn take_frame_buffer(&mut self) -> Result<Option<Vec<u8>>, Error> {
+        if let Some(mut buf) = self.frame.take() {
+            let st = unsafe { rrte_hip_host_unregister(self.ctx, buf.as_mut_ptr() as *mut c_void) };
+            if st != RRTE_OK {
+                self.frame = Some(buf);
+                return Err(self.check(st).unwrap_err());
+            }
+            return Ok(Some(buf));
+        }
+        Ok(None)
+    }
+
+    /// Raytracer::render into the pinned frame buffer (set_frame_buffer): the frame's W*H*4 bytes.
+    pub fn render_pinned(&mut self, scene: &SceneIr, params: &rrte_render_params) -> Result<&[u8], Error> {
+        let need = params.width as usize * params.height as usize * 4;
+        let ctx = self.ctx;
+        let ptr = match self.frame.as_mut() {
+            Some(b) if b.len() >= need => b.as_mut_ptr(),
+            _ => return Err(Error { status: RRTE_INVALID_ARG, message: format!("no pinned frame buffer of {need} bytes") }),
+        };
+        let ir = scene.raw();
+        self.check(unsafe { rrte_hip_render(ctx, &ir, params, ptr) })?;
+        Ok(&self.frame.as_ref().unwrap()[..need])
+    }
+
+    /// The device code's build id (rrte_hip_build_id: device headers, hiprtc options and version).
+    pub fn build_id() -> Result<String, Error> {
+        let mut buf = [0 as c_char; 64];
+        let st = unsafe { rrte_hip_build_id(buf.as_mut_ptr(), buf.len()) };
+        if st != RRTE_OK {
+            return Err(Error { status: st, message: "rrte_hip_build_id failed".into() });
+        }
+        Ok(unsafe { CStr::from_ptr(buf.as_ptr()) }.to_string_lossy().into_owned())
     }
 
     /// Statistics of the last frame (rays cast, kernel time, gather time, upload time).
