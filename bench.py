@@ -60,9 +60,10 @@ def parse():
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
                          "so one frame's tail overlaps the next frame's start (1 = strictly one after another); "
                          "default 4 on one GPU (tools/runs/r02_inflight.sh); N > 1: frames per gather batch, default 8")
-    ap.add_argument("--streams", type=int, default=4,
-                    help="N > 1: caller streams the frames rotate over (each frame is launched at its call on its "
-                         "stream; frames in flight), independent of the gather batch (--inflight)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="N > 1: caller streams the frames rotate over, independent of the gather batch "
+                         "(--inflight); 1 with multi-frame batch launches (the library renders on its own streams), "
+                         "e.g. 4 with RRTE_BATCH_LAUNCH=0 (each frame launched at its call on its caller's stream)")
     ap.add_argument("--flyby", type=int, default=0,
                     help="camera fly-by: frame i renders camera pose i %% K of K poses orbiting the scene's target "
                          "(0.6 degrees apart; pose 0 = the scene's own camera); 0 = static camera")
@@ -341,12 +342,11 @@ def main():
             c2.transform.position = vec3(dx * math.cos(a) - dz * math.sin(a), p0[1], dx * math.sin(a) + dz * math.cos(a))
             c2.look_at((0.0, 2.0, 0.0))
             poses.append(LoweredScene(objs, lights, c2))
-    # N > 1: every frame is launched at its call on one of --streams caller streams (frames in flight)
-    # -- rank 0 writing its own bands straight into the frame buffers, the peers into their send slabs
-    # -- and the frames are exchanged in batches of F (rrte_hip_set_gather_batch): ONE grouped
-    # ncclSend / ncclRecv per batch on the library's comm stream moves the peers' RGB24 rows to rank 0,
-    # which expands them.  Every frame is still composed on rank 0 inside the timed
-    # region (the last batch is flushed before its end).
+    # N > 1: frames are exchanged in batches of F (rrte_hip_set_gather_batch): each batch renders in
+    # multi-frame launches (8 frames per launch) on the library's render streams -- rank 0 writing its
+    # own bands straight into the frame buffers -- and ONE grouped ncclSend / ncclRecv per batch on its
+    # comm stream moves the peers' RGB24 rows to rank 0, which expands them.  Every
+    # frame is still composed on rank 0 inside the timed region (the last batch is flushed before its end).
     ctx = Context(local_rank, jit={"off": abi.JIT_OFF, "on": abi.JIT_ON, "auto": abi.JIT_AUTO}[args.jit])
     lib = ctx.lib
 
@@ -382,7 +382,8 @@ def main():
     def step(i=0):
         j = i % F
         if gath:
-            # each frame launched at its call on caller stream i % NS; the exchange is batched
+            # batched frames render on the library's own streams (multi-frame launches at the batch's
+            # close); one caller stream keeps the batch's dependency on its callers to one event
             st = render_gather(h, srefs[i % K], pref, 0, fptrs[j] if rank == 0 else None, sptrs[i % NS])
         else:
             st = render_async(h, srefs[i % K], pref, fptrs[j], None, sptrs[j])

@@ -214,10 +214,12 @@ struct rrte_ctx {
     uint64_t scene_gen = 0;       // bumped whenever the cached scene changes
     uint32_t scene_feat = kFeatAll;  // the cached scene's features (kFeat*): its generic kernel variant
     bool env_generic_all = false;    // RRTE_GENERIC_ALL=1: the all-features generic kernel for every scene (A/B, tests)
-    // Batched gathers render each frame at its call (its own launch on the caller's stream: the root
-    // in place, a peer into its slot of the send slab) and only the exchange is batched; RRTE_BATCH_LAUNCH=1
-    // keeps round 4's multi-frame launches at the batch's close (A/B)
-    bool env_batch_launch = false;
+    // Batched gathers render the batch's frames in multi-frame launches at its close (default), or with
+    // RRTE_BATCH_LAUNCH=0 each frame at its call (its own launch on the caller's stream: the root in
+    // place, a peer into its slot of the send slab) with only the exchange batched -- measured slower
+    // for rank shares (a launch of 1/N of a frame lasts as long as its slowest tile, so
+    // per-frame launches are tail-bound; 8 frames per launch overlap their tails)
+    bool env_batch_launch = true;
     // Blocking drop-in path into PINNED host memory (hipHostMalloc'd by the caller, or registered with
     // rrte_hip_host_register): the kernel stores the frame straight into the caller's buffer over PCIe
     // while it renders, instead of a render followed by one 8.3 MB D2H copy.  RRTE_BND_ZEROCOPY=0 turns
@@ -1854,7 +1856,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_TILE_XCD")) c->env_tile_xcd = g[0] == '1';
     if (const char* g = getenv("RRTE_PRIO_SLOTS")) c->env_prio_slots = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
-    if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] == '1';
+    if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] != '0';
     if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
     if (const char* g = getenv("RRTE_NOCOMM_WAIT_MS")) c->env_nocomm_wait_ms = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
