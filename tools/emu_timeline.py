@@ -16,7 +16,7 @@ for r in kt + ht:
 kt.sort(key=lambda r: r["s"])
 ht.sort(key=lambda r: r["s"])
 multi = [r for r in kt if ("rrte_jit_kernel" in r["Kernel_Name"] or "ray_kernel" in r["Kernel_Name"])
-         and int(r.get("Grid_Size_Y") or r.get("Grid_Size", "0").split(",")[0] if False else r.get("Grid_Size_Y") or 1) > 1]
+         and int(r.get("Grid_Size_Y") or 1) > 1]
 win = multi[-nb:]
 corr = {r["Correlation_Id"]: r for r in ht}
 first_api = corr.get(win[0]["Correlation_Id"])
