@@ -250,6 +250,13 @@ struct rrte_ctx {
                                  // de-interleave, 4 no comm-stream waits -- results are wrong
     double hp[10] = {};
     uint64_t hp_frames = 0;
+    // RRTE_TRACE=1 (diagnostics): every event record / stream wait / launch of the frame paths with its
+    // stream and event, host-timestamped, printed to stderr by rrte_hip_destroy (matched against a
+    // rocprofv3 kernel trace by launch order)
+    bool trace = false;
+    struct TraceRec { double us; const char* what; const void* st; const void* ev; uint32_t a, b; };
+    std::vector<TraceRec> trace_log;
+    std::chrono::steady_clock::time_point trace_t0 = std::chrono::steady_clock::now();
     // Tile order (KParams::hot).  Every kTileReprofile-th launch of one launch shape (size, rows, band
     // mapping, mode, kernel) times each tile of its frame 0 on the device and copies the durations back
     // asynchronously; once they have arrived, later launches of that shape dispatch every tile slowest
@@ -384,6 +391,20 @@ rrte_status fail(rrte_ctx* c, rrte_status st, const char* fmt, ...) {
             if (s_ != RRTE_OK) return s_;                                                          \
         }                                                                                          \
     } while (0)
+
+void trace_rec(rrte_ctx* c, const char* what, const void* st, const void* ev, uint32_t a = 0, uint32_t b = 0) {
+    if (!c->trace) return;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c->trace_t0).count();
+    c->trace_log.push_back({us, what, st, ev, a, b});
+}
+hipError_t ev_record(rrte_ctx* c, hipEvent_t ev, hipStream_t st, const char* tag) {
+    trace_rec(c, tag, st, ev);
+    return hipEventRecord(ev, st);
+}
+hipError_t ev_wait(rrte_ctx* c, hipStream_t st, hipEvent_t ev, const char* tag) {
+    trace_rec(c, tag, st, ev);
+    return hipStreamWaitEvent(st, ev, 0);
+}
 
 // Device buffer of at least n elements; a smaller one goes to the graveyard (launches in flight may
 // still read it; freed when the context is next idle).
@@ -1559,7 +1580,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     if (!tp.slots.empty() && tp.slots.size() == tiles && (tp.cur >= 0 || upload_hot_list(c, tp))) {
         auto& ord = tp.ordered[tp.cur];  // (first launch of this stream on the version: after its upload)
         if (tp.ev_up[tp.cur] && std::find(ord.begin(), ord.end(), st) == ord.end()) {
-            if (hipStreamWaitEvent(st, tp.ev_up[tp.cur], 0) != hipSuccess) return false;
+            if (ev_wait(c, st, tp.ev_up[tp.cur], "wait tile-list upload") != hipSuccess) return false;
             ord.push_back(st);
         }
         k.hot = tp.d_list[tp.cur];
@@ -1592,7 +1613,7 @@ rrte_status finish_tile_order(rrte_ctx* c, const LaunchPlan& L, bool profile, hi
     auto& tp = c->tprof[L.prof];
     if (!profile) return RRTE_OK;
     HIPCHK(c, hipMemcpyAsync(tp.h_cost, tp.d_cost, (size_t)tp.tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipEventRecord(tp.ev, st));
+    HIPCHK(c, ev_record(c, tp.ev, st, "record tile-profile copy"));
     tp.pending = true;
     return RRTE_OK;
 }
@@ -1624,13 +1645,14 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
     if (c->sb_cur >= 0) {  // the launch reads the current scene version: after its upload, tracked until retired
         rrte_ctx::SceneBuf& B = c->sb[c->sb_cur];
         if (std::find(B.ordered.begin(), B.ordered.end(), st) == B.ordered.end()) {
-            HIPCHK(c, hipStreamWaitEvent(st, B.ev_up, 0));
+            HIPCHK(c, ev_wait(c, st, B.ev_up, "wait scene upload"));
             B.ordered.push_back(st);
         }
         B.ret.use(st);
     }
     c->launched.use(st);
     const dim3 grid(L.gx, L.k.nframes, L.gy), block(kBlockThreads);
+    trace_rec(c, profile ? "launch ray (profiled)" : "launch ray", st, nullptr, L.k.nframes, L.k.rows);
     if (jk) {
         unsigned long long* ctr = c->d_counters;
         MeshView mv = c->mesh_view;
@@ -1842,6 +1864,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* t = getenv("RRTE_TILE_CULL")) c->env_tile_cull = t[0] != '0';
     if (const char* g = getenv("RRTE_FORCE_GATHER")) c->env_force_gather = g[0] == '1';
     if (const char* g = getenv("RRTE_HOST_PROFILE")) c->host_prof = g[0] == '1';
+    if (const char* g = getenv("RRTE_TRACE")) c->trace = g[0] == '1';
     if (const char* g = getenv("RRTE_DIAG_SKIP")) c->env_diag_skip = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GATHER_RGB24")) c->env_gather_rgba = g[0] == '0';
     c->env_guard_leaves = env_guard_setting();
@@ -1910,6 +1933,10 @@ void rrte_hip_destroy(rrte_ctx* c) {
         fprintf(stderr, "rrte host profile (%llu gather frames, us/frame):", (unsigned long long)c->hp_frames);
         for (int i = 0; i < 9; ++i) fprintf(stderr, " %s %.2f", names[i], c->hp[i] / (double)c->hp_frames);
         fprintf(stderr, "\n");
+    }
+    if (c->trace) {
+        for (const auto& t : c->trace_log)
+            fprintf(stderr, "rrte trace %12.1f us  %-34s stream %p event %p  %u %u\n", t.us, t.what, t.st, t.ev, t.a, t.b);
     }
     (void)hipSetDevice(c->device);
     if (c->h_stall) __hip_atomic_store(c->h_stall, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // injected stall
@@ -2307,6 +2334,7 @@ bool slab_rgb24(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_par
 static rrte_status deinterleave(rrte_ctx* c, hipStream_t st, const uint8_t* gathered, const DeinterleaveTargets& t,
                                 uint32_t n, uint32_t width, uint32_t height, const BandMap& bm, bool rgb24,
                                 size_t rank_stride, size_t frame_stride, uint32_t skip_rank = ~0u) {
+    trace_rec(c, "launch expansion", st, nullptr, n, height);
     bool vec4 = width % 4u == 0;
     for (uint32_t j = 0; j < n; ++j) vec4 = vec4 && reinterpret_cast<uintptr_t>(t.full[j]) % 16u == 0;
     const uint32_t per = vec4 ? 1024u : 256u;  // pixels one workgroup moves per pass
@@ -2370,10 +2398,10 @@ static rrte_status render_batch(rrte_ctx* c, bool at_flush) {
     // the slab's previous batch (its gather reads the send slab)
     if (!(c->env_diag_skip & 4u))
         for (uint32_t i = 0; i < b.nsrc; ++i) {
-            HIPCHK(c, hipEventRecord(b.ev_src[i], b.src[i]));
-            HIPCHK(c, hipStreamWaitEvent(rs, b.ev_src[i], 0));
+            HIPCHK(c, ev_record(c, b.ev_src[i], b.src[i], "record src (render)"));
+            HIPCHK(c, ev_wait(c, rs, b.ev_src[i], "render waits src"));
         }
-    if (b.rendered == 0) HIPCHK(c, hipStreamWaitEvent(rs, c->ev_batch[k], 0));
+    if (b.rendered == 0) HIPCHK(c, ev_wait(c, rs, c->ev_batch[k], "render waits slab's last exchange"));
     hs.lap(2);
     // a copy of the batch's plan: b.plan's fields before KParams::nframes are the batch-compatibility
     // key gather_frame compares every new frame with, identically on every rank, so they stay as
@@ -2391,10 +2419,12 @@ static rrte_status render_batch(rrte_ctx* c, bool at_flush) {
         if (r != RRTE_OK) return r;
     }
     b.rendered = b.n;
-    HIPCHK(c, hipEventRecord(c->ev_render[k], rs));
+    HIPCHK(c, ev_record(c, c->ev_render[k], rs, "record render done"));
     hs.lap(3);
     return RRTE_OK;
 }
+
+__global__ void noop_kernel() {}
 
 // The stalled-peer stand-in of RRTE_FAULT_STALL_GATHER: spins on a host-written flag (vector atomic
 // loads at system scope) with its own 5 s deadline on the 100 MHz wall clock, so it always ends.
@@ -2544,14 +2574,14 @@ static rrte_status flush_batch(rrte_ctx* c) {
         if (launched_per_frame) {
             // the frames rendered on their callers' streams: the exchange follows each of them
             for (uint32_t i = 0; i < b.nsrc; ++i) {
-                HIPCHK(c, hipEventRecord(b.ev_src[i], b.src[i]));
-                HIPCHK(c, hipStreamWaitEvent(c->comm_stream, b.ev_src[i], 0));
+                HIPCHK(c, ev_record(c, b.ev_src[i], b.src[i], "record src (exchange)"));
+                HIPCHK(c, ev_wait(c, c->comm_stream, b.ev_src[i], "comm waits src"));
             }
         } else {
-            HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_render[k], 0));
+            HIPCHK(c, ev_wait(c, c->comm_stream, c->ev_render[k], "comm waits render"));
         }
         if (c->last_gather_stream && c->last_gather_stream != c->comm_stream)
-            HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->last_gather_ev, 0));
+            HIPCHK(c, ev_wait(c, c->comm_stream, c->last_gather_ev, "comm waits last gather"));
         hs.lap(4);
         if ((r = before_collective(c, c->comm_stream)) != RRTE_OK) return r;
         // every peer's slab to the root: grouped point-to-point (the root's own bands never move); with
@@ -2590,7 +2620,7 @@ static rrte_status flush_batch(rrte_ctx* c) {
                 return r;
         }
         hs.lap(6);
-        HIPCHK(c, hipEventRecord(c->ev_batch[k], c->comm_stream));
+        HIPCHK(c, ev_record(c, c->ev_batch[k], c->comm_stream, "record exchange done"));
         return RRTE_OK;
     };
     if ((r = issue()) != RRTE_OK) return comm_abort(c, ("batch gather failed: " + c->err).c_str());
@@ -2651,6 +2681,14 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_batch[i], hipEventDisableTiming));
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_render[i], hipEventDisableTiming));
             }
+            // one empty kernel on each new stream now: the runtime binds a stream to a hardware queue at
+            // its first dispatch, which must not happen inside a later frame's critical path
+            for (int i = 0; i < c->batch_slabs; ++i) {
+                hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, c->render_stream[i]);
+                HIPCHK(c, hipGetLastError());
+            }
+            hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, c->comm_stream);
+            HIPCHK(c, hipGetLastError());
             for (int i = 0; i < rrte_ctx::kMaxBatch; ++i)
                 HIPCHK(c, hipEventCreateWithFlags(&b.ev_src[i], hipEventDisableTiming));
         }

@@ -218,13 +218,14 @@ def _info(ctx):
 
 
 def _recoloured_frames(n):
-    """The same topology as _frames (sdf-showcase), another value: one material recoloured."""
-    from rrte_amd import LambertianMaterial
+    """The same topology and array counts as _frames (sdf-showcase), another value: a material
+    recoloured in place (a new material object would add a material record -- another count, which
+    closes a batch on every rank alike)."""
     from rrte_amd.math import Color
     out = []
     for i in range(n):
         objs, lights, cam, cfg = scenes.sdf_showcase(W, H)
-        objs[3].material = LambertianMaterial(Color(0.9, 0.3, 0.1, 1.0))
+        objs[3].material._albedo = Color(0.9, 0.3, 0.1, 1.0)
         out.append((LoweredScene(objs, lights, cam), cfg.lower()))
     return out
 
