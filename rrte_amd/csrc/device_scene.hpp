@@ -151,12 +151,14 @@ struct KParams {
     // independent (raytracer.rs:57-60), so any order renders the same bytes; this one starts the
     // frame's longest waves first instead of wherever image order puts them.
     uint32_t* tile_cost;     // non-null: frame 0's workgroups store their duration (100 MHz ticks) at [y * tiles_x + x]
-    const uint32_t* hot;     // device tile list (hot_n words; immutable while launches use it)
+    const uint32_t* hot;     // device tile list (immutable while launches use it)
     uint32_t tiles_x, hot_n;
-    // slots [0, prio_slots) of the list -- the slowest tiles -- raise their wave's issue priority
-    // (s_setprio): on a SIMD shared with cheap waves the frame's critical chains issue first (A/B
-    // switch RRTE_PRIO_SLOTS; 0 = off)
-    uint32_t prio_slots;
+    // The list is stored XCD-major: slot k at hot[(k & 7) * hot_stride + (k >> 3)].  Workgroups are
+    // dispatched round-robin over the 8 XCDs (slot k on XCD k mod 8 when the slot rows are a multiple
+    // of 8 tiles wide), and each XCD has its own L2: in slot order every 64-B line of the list held
+    // slots of all 8 XCDs, so every XCD fetched the whole list (~1 MB of HBM reads per 1080p launch,
+    // PMC FETCH_SIZE); XCD-major, each XCD reads only its own eighth.
+    uint32_t hot_stride;
     // Output rows: 0 = this launch's rows packed (row r at r * width, frame z at out + z * frame_stride),
     // 1 = at their image rows of frame z's own buffer cam[z].out (image_row(r) * width: a multi-GPU
     // root renders its own bands straight into the final frames; RGBA8 only)

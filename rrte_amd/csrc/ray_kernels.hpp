@@ -2168,10 +2168,9 @@ __device__ __forceinline__ LaunchTile launch_tile(const KParams& kp) {
     if (kp.hot) {
         const uint32_t k = blockIdx.z * kp.tiles_x + blockIdx.x;
         t.run = k < kp.hot_n;
-        const uint32_t h = kp.hot[t.run ? k : 0u];
+        const uint32_t h = kp.hot[t.run ? (k & 7u) * kp.hot_stride + (k >> 3) : 0u];
         t.x = hot_x(h);
         t.y = hot_y(h);
-        if (k < kp.prio_slots) __builtin_amdgcn_s_setprio(2);
     }
     return t;
 }

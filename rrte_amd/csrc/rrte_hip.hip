@@ -311,9 +311,7 @@ struct rrte_ctx {
     hipEvent_t ev_bcopy = nullptr;
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed scrambled permutation of the tiles (tests)
-    bool env_tile_xcd = false;          // RRTE_TILE_XCD=1: XCD-aware LPT (lpt_slots_xcd; A/B experiment)
     uint32_t env_nocomm_wait_ms = 0;    // RRTE_NOCOMM_WAIT_MS: limit of device waits without a communicator (0 = none)
-    uint32_t env_prio_slots = 0;        // RRTE_PRIO_SLOTS=N: the list's first N slots raise wave priority (A/B)
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
     // per launch, so the version pool wraps within a few frames)
     bool env_test_recycle = false;
@@ -1404,33 +1402,6 @@ std::vector<uint32_t> lpt_slots(const uint32_t* costs, uint32_t n, uint32_t tile
     return slots;
 }
 
-// XCD-aware LPT (RRTE_TILE_XCD=1, A/B experiment): the four tiles of a tile row that share each 128-B
-// line of the frame (32 RGBA8 pixels) take slots k, k+8, k+16, k+24 -- workgroups b and b+8 share an
-// XCD under round-robin dispatch (MI355X_MICROARCH.md; for speed only, never for correctness) and
-// start together -- with the groups in LPT order of their slowest tile.  Every tile once.
-std::vector<uint32_t> lpt_slots_xcd(const uint32_t* costs, uint32_t n, uint32_t tiles_x) {
-    std::vector<uint32_t> slots;
-    if (n == 0 || tiles_x == 0) return slots;
-    const uint32_t gx = (tiles_x + 3u) / 4u, rows = n / tiles_x, ng = gx * rows;
-    std::vector<uint32_t> gcost(ng, 0u), order(ng);
-    for (uint32_t i = 0; i < n; ++i) {
-        uint32_t& g = gcost[(i / tiles_x) * gx + (i % tiles_x) / 4u];
-        g = std::max(g, costs[i]);
-    }
-    for (uint32_t g = 0; g < ng; ++g) order[g] = g;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return gcost[a] > gcost[b]; });
-    slots.reserve(n);
-    for (uint32_t base = 0; base < ng; base += 8u) {
-        const uint32_t m = std::min(8u, ng - base);
-        for (uint32_t i = 0; i < 4u; ++i)
-            for (uint32_t j = 0; j < m; ++j) {
-                const uint32_t g = order[base + j], x = (g % gx) * 4u + i;
-                if (x < tiles_x) slots.push_back(hot_pack(x, g / gx));
-            }
-    }
-    return slots;
-}
-
 // RRTE_TILE_ORDER=2 (tests): every tile once in a fixed scrambled order -- slot k takes tile
 // (k * stride) mod n for a stride near 0.618 n coprime with n -- so the list path runs on every launch
 // without a profile.
@@ -1445,6 +1416,9 @@ std::vector<uint32_t> fixed_slots(uint32_t n, uint32_t tiles_x) {
     }
     return slots;
 }
+
+// Words per XCD of a tile list of n slots stored XCD-major (KParams::hot_stride).
+uint32_t hot_stride(uint32_t n) { return (n + 7u) / 8u; }
 
 // Allocates what an upload of up to `words` list words needs -- pinned staging, the upload stream and
 // the device versions not yet allocated -- at profile time, so the first upload (inside a later render
@@ -1485,7 +1459,8 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
     }
     if (pick < 0) return false;
     tp.ret[pick].nev = 0;
-    const size_t words = tp.slots.size();
+    const size_t n = tp.slots.size(), stride = hot_stride((uint32_t)n);
+    const size_t words = 8u * stride;  // XCD-major (KParams::hot_stride)
     const size_t bytes = words * sizeof(uint32_t);
     if (tp.cap_list[pick] < words) {  // a larger frame: its launches have completed, the old buffer is idle
         if (tp.d_list[pick]) c->graveyard.push_back(tp.d_list[pick]);
@@ -1495,7 +1470,7 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
         tp.cap_list[pick] = words;
     }
     if (!reserve_hot_lists(tp, words)) return false;
-    memcpy(tp.h_list, tp.slots.data(), bytes);
+    for (size_t k = 0; k < n; ++k) tp.h_list[(k & 7u) * stride + (k >> 3)] = tp.slots[k];
     if (!tp.ev_up[pick] && hipEventCreateWithFlags(&tp.ev_up[pick], hipEventDisableTiming) != hipSuccess) return false;
     if (!tp.ev_stage && hipEventCreateWithFlags(&tp.ev_stage, hipEventDisableTiming) != hipSuccess) return false;
     if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
@@ -1516,7 +1491,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     k.tiles_x = L.gx;
     k.hot = nullptr;
     k.hot_n = 0;
-    k.prio_slots = 0;
+    k.hot_stride = 0;
     k.tile_cost = nullptr;
     // (RRTE_DEBUG bit 5 runs one workgroup in image-order numbering: no tile order; bit 4's per-wave
     // stamps work with it)
@@ -1534,10 +1509,8 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
             // counting sort takes ~0.5 ms of host time that a render call must not stall for
             std::vector<uint32_t> costs(tp.h_cost, tp.h_cost + tp.tiles);
             const uint32_t tx = tp.tiles_x;
-            const bool xcd = c->env_tile_xcd;
-            tp.work = std::async(std::launch::async, [key, costs = std::move(costs), tx, xcd]() {
-                return TilePlanResult{key, xcd ? lpt_slots_xcd(costs.data(), (uint32_t)costs.size(), tx)
-                                               : lpt_slots(costs.data(), (uint32_t)costs.size(), tx)};
+            tp.work = std::async(std::launch::async, [key, costs = std::move(costs), tx]() {
+                return TilePlanResult{key, lpt_slots(costs.data(), (uint32_t)costs.size(), tx)};
             });
             tp.working = true;
             tp.launches = 0;
@@ -1585,7 +1558,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         }
         k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
-        k.prio_slots = std::min(c->env_prio_slots, k.hot_n);
+        k.hot_stride = hot_stride(k.hot_n);
         tp.ret[tp.cur].use(st);
     }
     if (!profile) return false;
@@ -1599,7 +1572,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         tp.cap_h = tiles;
     }
     if (!tp.ev && hipEventCreateWithFlags(&tp.ev, hipEventDisableTiming) != hipSuccess) return false;
-    if (!reserve_hot_lists(tp, tiles)) return false;
+    if (!reserve_hot_lists(tp, 8u * (size_t)hot_stride(tiles))) return false;
     k.tile_cost = tp.d_cost;  // every tile of frame 0 stores its duration (no clearing needed)
     tp.cam_sig = cam;
     tp.pending_key = key;
@@ -1876,8 +1849,6 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_BAND_SKY")) c->env_band_sky = g[0] != '0';
     if (const char* g = getenv("RRTE_COMM_PRIORITY")) c->env_comm_priority = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
-    if (const char* g = getenv("RRTE_TILE_XCD")) c->env_tile_xcd = g[0] == '1';
-    if (const char* g = getenv("RRTE_PRIO_SLOTS")) c->env_prio_slots = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
     if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] != '0';
     if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
