@@ -283,9 +283,10 @@ struct rrte_ctx {
         Retire ret[kVersions];
         hipEvent_t ev_up[kVersions] = {};                 // the version's upload copy done
         std::vector<hipStream_t> ordered[kVersions];     // streams already made to wait for ev_up
-        uint32_t* h_list = nullptr;      // pinned staging (reused once the last upload's copy is done)
-        size_t cap_h_list = 0;
-        hipEvent_t ev_stage = nullptr;   // the last upload's copy out of h_list done
+        // pinned staging, one per version: a version's staging is rewritten only when the version is
+        // reused, i.e. after every launch that read it -- each of which waited for its copy (ev_up)
+        uint32_t* h_list[kVersions] = {};
+        size_t cap_h_list[kVersions] = {};
         hipStream_t upload_stream = nullptr;
         int cur = -1;                    // version holding `slots` (-1: not uploaded)
         uint64_t launches = 0;           // launches of `key` since its last profile
@@ -1424,16 +1425,18 @@ uint32_t hot_stride(uint32_t n) { return (n + 7u) / 8u; }
 // the device versions not yet allocated -- at profile time, so the first upload (inside a later render
 // call) allocates nothing.
 bool reserve_hot_lists(rrte_ctx::TileProfile& tp, size_t words) {
-    if (tp.cap_h_list < words) {
-        // (pinned staging: the last copy out of it must be done -- the upload stream holds copies only)
-        if (tp.ev_stage && hipEventSynchronize(tp.ev_stage) != hipSuccess) return false;
-        if (tp.h_list) (void)hipHostFree(tp.h_list);
-        tp.h_list = nullptr;
-        tp.cap_h_list = 0;
-        if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_list), words * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
-            return false;
-        tp.cap_h_list = words;
-    }
+    for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i)
+        if (tp.cap_h_list[i] < words && i != tp.cur) {
+            // (a version other than the current one: every launch that read it -- and its copy -- is
+            // done before it is reused; the current version's staging grows at its next reuse)
+            if (!retired_done(tp.ret[i])) continue;
+            if (tp.h_list[i]) (void)hipHostFree(tp.h_list[i]);
+            tp.h_list[i] = nullptr;
+            tp.cap_h_list[i] = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_list[i]), words * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+                return false;
+            tp.cap_h_list[i] = words;
+        }
     if (!tp.upload_stream && hipStreamCreateWithFlags(&tp.upload_stream, hipStreamNonBlocking) != hipSuccess) return false;
     for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i)
         if (!tp.d_list[i]) {
@@ -1450,8 +1453,6 @@ bool reserve_hot_lists(rrte_ctx::TileProfile& tp, size_t words) {
 // version after it (plan_tile_order), so every launch sees a whole list and no render call waits.
 bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
     constexpr int K = rrte_ctx::TileProfile::kVersions;
-    // the staging buffer still feeds the previous upload's copy: keep the current list for now
-    if (tp.ev_stage && hipEventQuery(tp.ev_stage) != hipSuccess) return false;
     int pick = -1;
     for (int k = 1; k <= K && pick < 0; ++k) {  // the oldest retired version first
         const int v = (int)((tp.uploads + (uint64_t)k) % K);
@@ -1470,12 +1471,12 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
         tp.cap_list[pick] = words;
     }
     if (!reserve_hot_lists(tp, words)) return false;
-    for (size_t k = 0; k < n; ++k) tp.h_list[(k & 7u) * stride + (k >> 3)] = tp.slots[k];
+    if (tp.cap_h_list[pick] < words) return false;  // (reserve_hot_lists could not grow it yet)
+    uint32_t* stage = tp.h_list[pick];
+    for (size_t k = 0; k < n; ++k) stage[(k & 7u) * stride + (k >> 3)] = tp.slots[k];
     if (!tp.ev_up[pick] && hipEventCreateWithFlags(&tp.ev_up[pick], hipEventDisableTiming) != hipSuccess) return false;
-    if (!tp.ev_stage && hipEventCreateWithFlags(&tp.ev_stage, hipEventDisableTiming) != hipSuccess) return false;
-    if (hipMemcpyAsync(tp.d_list[pick], tp.h_list, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
-        hipEventRecord(tp.ev_up[pick], tp.upload_stream) != hipSuccess ||
-        hipEventRecord(tp.ev_stage, tp.upload_stream) != hipSuccess)
+    if (hipMemcpyAsync(tp.d_list[pick], stage, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
+        hipEventRecord(tp.ev_up[pick], tp.upload_stream) != hipSuccess)
         return false;
     tp.ordered[pick].clear();
     if (tp.cur >= 0 && retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
@@ -1944,10 +1945,10 @@ void rrte_hip_destroy(rrte_ctx* c) {
             if (tp.d_list[i]) (void)hipFree(tp.d_list[i]);
             destroy_events(tp.ret[i]);
         }
-        if (tp.h_list) (void)hipHostFree(tp.h_list);
+        for (uint32_t* h : tp.h_list)
+            if (h) (void)hipHostFree(h);
         for (hipEvent_t e : tp.ev_up)
             if (e) (void)hipEventDestroy(e);
-        if (tp.ev_stage) (void)hipEventDestroy(tp.ev_stage);
         if (tp.upload_stream) (void)hipStreamDestroy(tp.upload_stream);
     }
     for (int i = 0; i < rrte_ctx::kBndChunksMax; ++i) {
