@@ -1547,10 +1547,8 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     ++tp.launches;
     // RRTE_TEST_RECYCLE=1: a new list version every launch (the fixed list re-uploaded), so the
     // version pool wraps within kVersions launches
-    if (c->env_test_recycle && tp.fixed && tp.cur >= 0) {
-        if (retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
-        tp.cur = -1;
-    }
+    // (into a free version, retiring the current one; with none free the launch keeps the current list)
+    if (c->env_test_recycle && tp.fixed && tp.cur >= 0) (void)upload_hot_list(c, tp);
     if (!tp.slots.empty() && tp.slots.size() == tiles && (tp.cur >= 0 || upload_hot_list(c, tp))) {
         auto& ord = tp.ordered[tp.cur];  // (first launch of this stream on the version: after its upload)
         if (tp.ev_up[tp.cur] && std::find(ord.begin(), ord.end(), st) == ord.end()) {
