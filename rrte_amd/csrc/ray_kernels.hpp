@@ -76,6 +76,11 @@ __device__ __forceinline__ void static_for(F& f) {
         static_for<I + 1, N>(f);
     }
 }
+// The ten SDF leaf kinds (RRTE_SDF_SPHERE .. RRTE_SDF_ELLIPSOID) as compile-time constants.
+template <class F>
+__device__ __forceinline__ void static_for_leaves(F& f) {
+    static_for<RRTE_SDF_SPHERE, RRTE_SDF_ELLIPSOID + 1u>(f);
+}
 template <class S, class F>
 __device__ __forceinline__ void for_each_prim(const S& sc, F&& f) {
     if constexpr (S::kStatic) {
@@ -453,6 +458,38 @@ struct SdfProgramT {
     }
 };
 using SdfProgram = SdfProgramT<kFeatAll>;
+
+#ifndef RRTE_SDF_LEAF_DISPATCH
+#define RRTE_SDF_LEAF_DISPATCH 1  // generic kernel: one-leaf objects march with a compile-time leaf kind (A/B)
+#endif
+// A one-leaf program of the generic kernel with its leaf kind known at compile time: the runtime
+// scene dispatches on the leaf once per object (intersect_at), so the sphere-tracing loop runs that
+// leaf's straight-line distance, as a scene-specialised kernel does, with only the leaf's sizes read
+// (through scalar loads, hoisted out of the loop).  leaf_scale is sdf_leaf_scale of the one node.
+template <uint32_t OP>
+struct SdfLeafProgram {
+    static constexpr bool kSmall = true;
+    const rrte_sdf_node* __restrict__ node;
+    __device__ __forceinline__ float leaf_scale() const {
+        float k = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) k += node->f[j] < 0.0f ? -node->f[j] : node->f[j];
+        return k;
+    }
+    template <class G>
+    __device__ __forceinline__ float eval(f3 p, G& g) const { return sdf_leaf(g, OP, node->f, p); }
+    __device__ __forceinline__ float operator()(f3 p) const {
+        GuardNow g;
+        return eval(p, g);
+    }
+};
+// Leaves whose one-leaf program is convex and 1-Lipschitz whatever their sizes (sdf_convex; the cone
+// only for radius and height > 0, a runtime fact, so not here): the secant early miss applies.
+template <uint32_t OP>
+constexpr bool leaf_convex() {
+    return OP == RRTE_SDF_SPHERE || OP == RRTE_SDF_BOX || OP == RRTE_SDF_CYLINDER || OP == RRTE_SDF_PRISM ||
+           OP == RRTE_SDF_CAPSULE;
+}
 
 // Is the postfix program a convex, 1-Lipschitz function of p?  Convex leaves (exact SDFs of convex
 // solids -- the signed distance of a convex set is a supremum of affine functions -- and the prism's
@@ -1220,9 +1257,22 @@ __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray&
     // (a kind outside the variant's features cannot occur: the host picked the variant from the scene)
     if (pr.kind == RRTE_PRIM_SPHERE) return isect_sphere<NEED_HIT, ANY>(pr, r, t_min, t_max, out);
     if constexpr ((F & kFeatSdf) != 0u)
-        if (pr.kind == RRTE_PRIM_SDF)
-            return isect_sdf<NEED_HIT, SdfProgramT<F>, ANY>(pr, SdfProgramT<F>{sc.nodes + pr.sdf_first, pr.sdf_count},
-                                                            r, t_min, t_max, out);
+        if (pr.kind == RRTE_PRIM_SDF) {
+            const rrte_sdf_node* nd = sc.nodes + pr.sdf_first;
+            if (RRTE_SDF_LEAF_DISPATCH && pr.sdf_count == 1u) {
+                bool hit = false;
+                auto leaf = [&](auto opc) {
+                    constexpr uint32_t OP = decltype(opc)::value;
+                    if (nd->op == OP)
+                        hit = isect_sdf<NEED_HIT, SdfLeafProgram<OP>, ANY,
+                                        (ANY ? kSecantExit >= 1 : kSecantExit >= 2) && leaf_convex<OP>()>(
+                            pr, SdfLeafProgram<OP>{nd}, r, t_min, t_max, out);
+                };
+                static_for_leaves(leaf);
+                return hit;
+            }
+            return isect_sdf<NEED_HIT, SdfProgramT<F>, ANY>(pr, SdfProgramT<F>{nd, pr.sdf_count}, r, t_min, t_max, out);
+        }
     if constexpr ((F & kFeatAnalytic) != 0u) {
         switch (pr.kind) {
         case RRTE_PRIM_PLANE: return isect_plane<NEED_HIT>(pr, r, t_min, t_max, out);
@@ -1314,7 +1364,16 @@ __device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray
     }
     if constexpr ((F & kFeatSdf) != 0u) {
         if (pr.kind == RRTE_PRIM_SDF) {
-            sdf_hit_attributes(SdfProgramT<F>{sc.nodes + pr.sdf_first, pr.sdf_count}, r, t, out);
+            const rrte_sdf_node* nd = sc.nodes + pr.sdf_first;
+            if (RRTE_SDF_LEAF_DISPATCH && pr.sdf_count == 1u) {
+                auto leaf = [&](auto opc) {
+                    constexpr uint32_t OP = decltype(opc)::value;
+                    if (nd->op == OP) sdf_hit_attributes(SdfLeafProgram<OP>{nd}, r, t, out);
+                };
+                static_for_leaves(leaf);
+                return;
+            }
+            sdf_hit_attributes(SdfProgramT<F>{nd, pr.sdf_count}, r, t, out);
             return;
         }
     }
