@@ -13,6 +13,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import shutil
 import statistics
 import sys
 import time
@@ -230,6 +231,52 @@ def measured_valu_peak():
     return {"fma_add_mul": fma, "cmp_select_max": sel, "source": "profiles/r01_valu_peak.json"}
 
 
+def auto_cold_start(scene, prm, fulls, sptrs, dev, rays_per_frame, limit_s=8.0):
+    """The default JIT policy (RRTE_JIT_AUTO) from a cold start -- a new context and an empty code-object
+    cache, as a drop-in user's first run: frames rendered back to back (frames in flight as the
+    headline) on the generic kernel while the scene-specialised kernel compiles in the background,
+    until it takes over.  Reports the time to the switch, the generic frames rendered meanwhile and
+    their rate, and the hiprtc compile time (a cache miss)."""
+    import tempfile
+
+    import torch
+    F = len(fulls)
+    tmp = tempfile.mkdtemp(prefix="rrte_jit_cold_")
+    old = os.environ.get("RRTE_JIT_CACHE_DIR")
+    os.environ["RRTE_JIT_CACHE_DIR"] = tmp  # (read by the background compile too)
+    try:
+        c = Context(dev.index, jit=abi.JIT_AUTO)
+        t0 = time.perf_counter()
+        n, switch = 0, None
+        while time.perf_counter() - t0 < limit_s:
+            c.check(c.lib.rrte_hip_render_async(c.h, scene.ref(), C.byref(prm), fulls[n % F].data_ptr(), None,
+                                                sptrs[n % F]))
+            n += 1
+            if n % F == 0:
+                torch.cuda.synchronize(dev)
+                if c.stats().jit_active:
+                    switch = (time.perf_counter() - t0, n)
+                    break
+        torch.cuda.synchronize(dev)
+        st = c.stats()
+        c.close()
+    finally:
+        if old is None:
+            os.environ.pop("RRTE_JIT_CACHE_DIR", None)
+        else:
+            os.environ["RRTE_JIT_CACHE_DIR"] = old
+        shutil.rmtree(tmp, ignore_errors=True)
+    if switch is None:
+        return {"switched": False, "seconds": round(limit_s, 2), "generic_frames": n}
+    gen = max(1, switch[1] - F)  # (the last in-flight group ran on the specialised kernel)
+    return {"switched": True, "ms_to_specialised": round(switch[0] * 1e3, 1), "generic_frames": gen,
+            "generic_ms_per_frame": round(switch[0] * 1e3 / gen, 4),
+            "generic_Mray_s": round(rays_per_frame / (switch[0] / gen) / 1e6, 1),
+            "jit_compile_ms": round(st.jit_compile_ms, 1),
+            "note": "new context, empty code-object cache (RRTE_JIT_CACHE_DIR=fresh dir): frames on the generic "
+                    "kernel until the background hiprtc compile lands (include/rrte_hip.h RRTE_JIT_AUTO)"}
+
+
 def kernel_variants(scene, prm, fulls, sptrs, dev, rays_per_frame, anim=None, n=60):
     """Secondary throughput of the headline workload per kernel kind (rank 0, N=1; not the headline):
     the generic kernel, the TOPOLOGY specialisation (structure compiled in, values read from the
@@ -275,6 +322,7 @@ def kernel_variants(scene, prm, fulls, sptrs, dev, rays_per_frame, anim=None, n=
             out[kind]["scenes"] = len(frames)
             out[kind]["upload_host_ms"] = round(st.upload_ms, 4)
         c.close()
+    out["auto_cold_start"] = auto_cold_start(scene, prm, fulls, sptrs, dev, rays_per_frame)
     if "topology_animated" in out:
         out["topology_animated"]["vs_static_topology"] = round(
             out["topology_animated"]["ms_per_frame"] / out["topology"]["ms_per_frame"], 4)
