@@ -159,6 +159,10 @@ struct KParams {
     // slots of all 8 XCDs, so every XCD fetched the whole list (~1 MB of HBM reads per 1080p launch,
     // PMC FETCH_SIZE); XCD-major, each XCD reads only its own eighth.
     uint32_t hot_stride;
+    // Tile shape of 64-thread workgroups: 1 << tile_shift pixels wide, 64 >> tile_shift rows (3: the 8x8
+    // tiles of every frame path; 5: 32x2, each wave storing two whole 128-B lines of RGBA8 -- the
+    // blocking path's zero-copy stores into pinned host memory cross PCIe as full lines)
+    uint32_t tile_shift;
     // Output rows: 0 = this launch's rows packed (row r at r * width, frame z at out + z * frame_stride),
     // 1 = at their image rows of frame z's own buffer cam[z].out (image_row(r) * width: a multi-GPU
     // root renders its own bands straight into the final frames; RGBA8 only)

@@ -2198,20 +2198,24 @@ __device__ __forceinline__ uint32_t camera_tile_mask(const KParams& kp, const Fr
                                                      uint32_t ty) {
     const uint32_t sh = cm.tile_cull;
     if (!sh) return ~0u;
-    uint32_t bx, by;
-    if (kWg64) {  // one 8x8 tile per workgroup
-        bx = (tx * 8u) >> sh;
-        by = image_row(kp, ty * 8u) >> sh;
+    uint32_t bx, bx1, by;
+    if (kWg64) {  // one tile per workgroup: (1 << tile_shift) x (64 >> tile_shift) pixels
+        // (its rows lie in one 8-row block of consecutive image rows: 64 >> tile_shift divides 8 and
+        // band heights are multiples of 8)
+        bx = (tx << kp.tile_shift) >> sh;
+        bx1 = ((tx << kp.tile_shift) + (1u << kp.tile_shift) - 1u) >> sh;
+        by = image_row(kp, ty * (64u >> kp.tile_shift)) >> sh;
     } else {
         const uint32_t wave = sh == 3u ? (threadIdx.x >> 6) : 0u;
         bx = (blockIdx.x * 16u + (wave & 1u) * 8u) >> sh;
+        bx1 = bx;
         by = image_row(kp, blockIdx.y * 16u + (wave >> 1) * 8u) >> sh;
     }
     const uint32_t j = threadIdx.x & 63u;
     bool in = false;
-    if (j < cm.tile_n) {
+    if (j < cm.tile_n) {  // the rectangle meets the tile's blocks [bx, bx1] x by
         const uint32_t t = cm.tile_rect[j];
-        in = bx >= (t & 255u) && bx <= ((t >> 8) & 255u) && by >= ((t >> 16) & 255u) && by <= (t >> 24);
+        in = bx1 >= (t & 255u) && bx <= ((t >> 8) & 255u) && by >= ((t >> 16) & 255u) && by <= (t >> 24);
     }
     const uint32_t m = (uint32_t)__ballot(in);
     return m | (cm.tile_n < 32u ? (~0u << cm.tile_n) : 0u);  // objects past the table: never culled
@@ -2260,8 +2264,9 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     if ((kp.debug & 32u) && brow * tiles_x + tile.x != (kp.debug >> 16)) return;
     const bool timed = stamps || (kp.tile_cost && tile.z == 0u);
     const uint64_t t_wave0 = timed ? wall_clock64() : 0ull;
-    const uint32_t x = kWg64 ? tile.x * 8u + (lane & 7u) : tile.x * 16u + (wave & 1u) * 8u + (lane & 7u);
-    const uint32_t lr = kWg64 ? brow * 8u + (lane >> 3) : brow * 16u + (wave >> 1) * 8u + (lane >> 3);
+    const uint32_t ts = kp.tile_shift;  // (kWg64: tile 1 << ts wide, 64 >> ts rows)
+    const uint32_t x = kWg64 ? (tile.x << ts) + (lane & ((1u << ts) - 1u)) : tile.x * 16u + (wave & 1u) * 8u + (lane & 7u);
+    const uint32_t lr = kWg64 ? brow * (64u >> ts) + (lane >> ts) : brow * 16u + (wave >> 1) * 8u + (lane >> 3);
     const bool live = x < kp.width && lr < kp.rows;
     const uint32_t xc = live ? x : 0u;
     const uint32_t y = image_row(kp, live ? lr : 0u);

@@ -225,6 +225,8 @@ struct rrte_ctx {
     // while it renders, instead of a render followed by one 8.3 MB D2H copy.  RRTE_BND_ZEROCOPY=0 turns
     // it off (A/B).  Pageable buffers keep the copy.
     bool env_bnd_zerocopy = true;
+    uint32_t tile_shift = 3;          // tile shape of the launch being planned (KParams::tile_shift)
+    uint32_t zc_tile_shift = 5;       // ... of zero-copy blocking frames (RRTE_ZC_TILE_SHIFT: 3 / 4 / 5)
     struct HostReg { void* p; size_t bytes; };
     std::vector<HostReg> host_regs;   // rrte_hip_host_register'ed ranges (unregistered at destroy)
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, valid; JitKernel* k; } jit_last{};
@@ -1313,6 +1315,12 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
     return k;
 }
 
+// Tile rows of a launch of `rows` rows (KParams::tile_shift: tiles 64 >> tile_shift rows high).
+uint32_t tile_grid_rows(const KParams& k, uint32_t rows) {
+    const uint32_t th = 64u >> k.tile_shift;
+    return (rows + th - 1u) / th;
+}
+
 LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint32_t rows,
                        uint32_t internal_flags, uint32_t row0 = 0u, const BandMap* bm = nullptr) {
     LaunchPlan L;
@@ -1332,8 +1340,9 @@ LaunchPlan plan_launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_pa
     L.num_prims = s->num_prims;
     L.num_lights = s->num_lights;
     L.num_materials = s->num_materials;
-    L.gx = (p->width + 7) / 8;  // one 8x8 tile per 64-thread workgroup (kBlockThreads)
-    L.gy = (rows + 7) / 8;
+    L.k.tile_shift = c->tile_shift;  // one tile per 64-thread workgroup (kBlockThreads): 8x8 unless overridden
+    L.gx = (p->width + (1u << L.k.tile_shift) - 1u) >> L.k.tile_shift;
+    L.gy = tile_grid_rows(L.k, rows);
     fill_tile_rects(c, s, p, L.k);
     return L;
 }
@@ -1500,7 +1509,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     auto& tp = c->tprof[L.prof];
     std::string key(reinterpret_cast<const char*>(&kern), sizeof kern);
     const uint32_t shape[] = {k.width, k.height, k.rows, k.row0, k.band_rows, k.nranks, k.rank, k.spp, k.max_depth,
-                              (uint32_t)L.mode, (uint32_t)L.cull, (uint32_t)L.single};
+                              (uint32_t)L.mode, (uint32_t)L.cull, (uint32_t)L.single, k.tile_shift};
     key.append(reinterpret_cast<const char*>(shape), sizeof shape);
     const uint32_t tiles = L.gx * L.gy;
     if (tp.pending && hipEventQuery(tp.ev) == hipSuccess) {
@@ -1763,7 +1772,9 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
         r = render_chunked(c, s, p, out8, (uint32_t)c->bnd_chunks);
     } else {
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        if (zc) c->tile_shift = c->zc_tile_shift;  // whole 128-B lines per wave across PCIe
         r = launch(c, s, p, p->height, zc ? zc : c->d_rgba, outf ? c->d_f32 : nullptr, c->stream);
+        c->tile_shift = 3;
         if (r == RRTE_OK) r = hipEventRecord(c->ev1, c->stream) == hipSuccess ? RRTE_OK : RRTE_HIP_ERROR;
     }
     c->nranks = nr;
@@ -1851,6 +1862,8 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
     if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] != '0';
     if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
+    if (const char* g = getenv("RRTE_ZC_TILE_SHIFT"))
+        c->zc_tile_shift = std::max(3u, std::min(5u, (uint32_t)strtoul(g, nullptr, 0)));
     if (const char* g = getenv("RRTE_NOCOMM_WAIT_MS")) c->env_nocomm_wait_ms = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
@@ -2333,7 +2346,7 @@ static rrte_status render_peers(rrte_ctx* c, const LaunchPlan& base, const Frame
         LaunchPlan L = base;
         L.k.rank = (uint32_t)q;
         L.k.rows = rows_for_rank(base.k.height, bm.band_rows, c->nranks, q, bm.sky, bm.root_bands, bm.peer_bands);
-        L.gy = (L.k.rows + 7) / 8;
+        L.gy = tile_grid_rows(L.k, L.k.rows);
         L.k.out_image_rows = 0u;
         L.k.frame_stride = frame_stride;
         L.prof = 1 + (q - 1) % rrte_ctx::kBndChunksMax;  // (a tile profile per peer shape)
