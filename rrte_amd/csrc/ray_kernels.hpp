@@ -1885,152 +1885,6 @@ __device__ __forceinline__ Col ray_color_ref(const S& sc, const KParams& kp, Ray
     return ps.out;
 }
 
-// Shadow-ray repacking (RRTE_SHADOW_REPACK, scene-specialised kernels).  The plain
-// shading loop casts light l's shadow rays from the lanes that hit a surface facing l: a wave whose
-// tile is partly sky or partly turned away runs every light's any-hit tests with idle lanes.  Here
-// the wave's (lane, light) pairs that cast are numbered light-major (q = prefix of the lights before
-// l + the lane's rank among l's casting lanes), and round r runs pairs [64r, 64r + 64) on all 64
-// lanes: lane i reads its pair's (source lane, light) from a per-wave LDS slot table, pulls the source's
-// hit point and normal with ds_bpermute and rebuilds that pair's shadow ray with the very operations
-// the source would use (illuminate's direction and distance for a point light, origin p + n * bias),
-// so each ray is bit-identical.  The any-hit test runs under the union of the round's lights' cull
-// masks (a superset: exact).  Each round's occlusion bits come back through one ballot, and the
-// contributions are then added per lane in light order, ambient lights included -- the reference's
-// summation order -- so the pixel is bit-identical to the plain loop.  Point and ambient lights only
-// (compile-time check); other scenes keep the plain loop.
-#ifndef RRTE_SHADOW_REPACK
-#define RRTE_SHADOW_REPACK 0
-#endif
-template <class S>
-constexpr bool repack_ok() {
-    if constexpr (!S::kStatic || S::num_lights < 2u || RRTE_MARCH_PRED != 0) {
-        return false;
-    } else {
-        bool ok = true;
-        uint32_t n = 0;
-        for (uint32_t i = 0; i < S::num_lights; ++i) {
-            uint32_t k = 0;
-            if constexpr (S::kTopo) k = S::topo_lights[i].kind;
-            else k = S::lights[i].kind;
-            if (k == RRTE_LIGHT_POINT) ++n;
-            else if (k != RRTE_LIGHT_AMBIENT) ok = false;
-        }
-        return ok && n >= 2u;
-    }
-}
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m below this lane
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ float pull(float v, uint32_t src) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute((int)(src << 2), __float_as_int(v)));
-}
-template <class S>
-__device__ __forceinline__ void shade_repacked(const S& sc, const KParams& kp, bool hit, const Hit& h, float ar, float ag,
-                                               float ab, const uint64_t* smask, float& cr, float& cg, float& cb,
-                                               uint32_t& nshadow) {
-    constexpr uint32_t nl = S::num_lights;
-    __shared__ uint32_t slots_all[nl * 64u * (kBlockThreads / 64u)];
-    uint32_t* slots = slots_all + (threadIdx.x >> 6) * (nl * 64u);
-    const uint32_t lane = threadIdx.x & 63u;
-    const float bias = kp.bias;
-    // phase A: which lanes cast a shadow ray to which light, and the pair numbering
-    // cast[l]: the lanes casting a ray to light l; cm[l]: those whose ray is tested (a light whose cull
-    // mask is empty can occlude nothing: its rays are counted and lit, not tested -- as occluded() does)
-    float fac[nl];
-    uint64_t cast[nl], cm[nl];
-    uint32_t pre[nl + 1];
-    pre[0] = 0u;
-    auto cast_of = [&](auto lii) {
-        constexpr uint32_t li = (uint32_t)decltype(lii)::value;
-        fac[li] = 0.0f;
-        cast[li] = cm[li] = 0ull;
-        if constexpr (light_kind<S, li>() == RRTE_LIGHT_POINT) {
-            bool c = false;
-            if (hit) {
-                const Contrib k = illuminate(light_at(sc, lii), h.p);
-                const float ndl = vdot(h.n, k.dir);
-                c = ndl > 0.0f && k.att > 0.0f;
-                fac[li] = k.att * ndl;
-            }
-            nshadow += c ? 1u : 0u;
-            cast[li] = __ballot(c);
-            cm[li] = smask[li] != 0ull ? cast[li] : 0ull;
-            if ((cm[li] >> lane) & 1ull) slots[pre[li] + lane_rank(cm[li])] = lane | (li << 8);
-        }
-        pre[li + 1] = pre[li] + (uint32_t)__builtin_popcountll(cm[li]);
-    };
-    static_for<0, nl>(cast_of);
-    const uint32_t pairs = pre[nl];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // phase B: the pairs in rounds of 64, every lane busy but the last round's tail
-    uint64_t occ_bits[nl] = {};
-    // (rounds unrolled at compile time: a loop let the compiler hoist the objects' constants out of it
-    // into VGPRs -- 101 registers against 52)
-    auto round = [&](auto rii) {
-        constexpr uint32_t r = (uint32_t)decltype(rii)::value;
-        if (r * 64u >= pairs) return;
-        const uint32_t q = r * 64u + lane;
-        const bool act = q < pairs;
-        const uint32_t e = slots[act ? q : 0u];
-        const uint32_t src = e & 63u, li = e >> 8;
-        const f3 p = V(pull(h.p.x, src), pull(h.p.y, src), pull(h.p.z, src));
-        const f3 n = V(pull(h.n.x, src), pull(h.n.y, src), pull(h.n.z, src));
-        f3 lpos = V(0.0f, 0.0f, 0.0f);
-        uint64_t mask = 0ull;
-        auto pick = [&](auto lii) {
-            constexpr uint32_t L = (uint32_t)decltype(lii)::value;
-            if constexpr (light_kind<S, L>() == RRTE_LIGHT_POINT) {
-                const DLight dl = light_at(sc, lii);
-                if (li == L) lpos = V(dl.position[0], dl.position[1], dl.position[2]);
-                if (pre[L] < r * 64u + 64u && pre[L + 1] > r * 64u) mask |= smask[L];  // (uniform)
-            }
-        };
-        static_for<0, nl>(pick);
-        bool occ = false;
-        if (act && !(kp.debug & 1u)) {
-            // illuminate's point-light direction and distance, and the shadow ray, as the source builds them
-            const f3 lv = vsub(lpos, p);
-            const float dist = vlen(lv);
-            const Ray sr = ray_new_unit(vadd(p, vmuls(n, bias)), vnorm(lv));
-            occ = occluded(sc, sr, bias, dist, mask);
-        }
-        occ_bits[r] = __ballot(occ);
-    };
-    static_for<0, nl>(round);
-    // phase C: the contributions per lane in light order (ambient lights included)
-    auto add = [&](auto lii) {
-        constexpr uint32_t li = (uint32_t)decltype(lii)::value;
-        const DLight l = light_at(sc, lii);
-        if constexpr (light_kind<S, li>() == RRTE_LIGHT_AMBIENT) {
-            if (hit) {
-                cr = cr + ar * l.cI[0];
-                cg = cg + ag * l.cI[1];
-                cb = cb + ab * l.cI[2];
-            }
-        } else {
-            if ((cast[li] >> lane) & 1ull) {
-                bool occ = false;
-                if ((cm[li] >> lane) & 1ull) {
-                    const uint32_t q = pre[li] + lane_rank(cm[li]);
-                    uint64_t bits = occ_bits[0];
-#pragma unroll
-                    for (uint32_t k = 1; k < nl; ++k) bits = (q >> 6) == k ? occ_bits[k] : bits;
-                    occ = (bits >> (q & 63u)) & 1ull;
-                }
-                if (!occ) {
-                    const float f = fac[li];
-                    cr = cr + ar * (l.cI[0] * f);
-                    cg = cg + ag * (l.cI[1] * f);
-                    cb = cb + ab * (l.cI[2] * f);
-                }
-            }
-        }
-    };
-    static_for<0, nl>(add);
-}
-
 // LAMBERT_SHADOW (build-defined) for one camera ray.  Called by
 // all 64 lanes of the wave (`live` marks the lanes that own a pixel): with
 // CULL the hit-point bound and the per-light shadow culls are wave reductions.
@@ -2126,15 +1980,8 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
                 auto cull_one = [&](auto lii) { smask[(uint32_t)lii] = shadow_cull(cl, hb, light_at(sc, lii), bnd); };
                 static_for<0, S::num_lights>(cull_one);
             }
-#if RRTE_SHADOW_REPACK
-            if constexpr (repack_ok<S>()) {
-                shade_repacked<S>(sc, kp, hit, h, ar, ag, ab, smask, cr, cg, cb, nshadow);
-            } else
-#endif
-            {
-                auto shade_one = [&](auto lii) { if (kShadeAll || hit) shade(light_at(sc, lii), smask[(uint32_t)lii], (uint32_t)lii); };
-                static_for<0, S::num_lights>(shade_one);
-            }
+            auto shade_one = [&](auto lii) { if (kShadeAll || hit) shade(light_at(sc, lii), smask[(uint32_t)lii], (uint32_t)lii); };
+            static_for<0, S::num_lights>(shade_one);
         } else {
             const float4 bnd = cull_on(cl) ? load_bound(cl) : float4{};
 #pragma unroll 1

@@ -1,13 +1,13 @@
 """Kernel variants behind build switches, each held to the parity bar against the oracle (linear image
-bit-exact, shadow-ray counts exact): the shadow-ray repacking of the scene-specialised kernel
-(RRTE_SHADOW_REPACK), the branch-free correctly rounded square root (RRTE_SQRT_BRANCHFREE; its
-exhaustive proof is tests/test_gpu_fpexact.py), and the generic kernel's all-features build next to
-the per-scene feature variants the host picks (RRTE_GENERIC_ALL)."""
-import numpy as np
+bit-exact, shadow-ray counts exact): the branch-free correctly rounded square root
+(RRTE_SQRT_BRANCHFREE; its exhaustive proof is tests/test_gpu_fpexact.py), and the generic kernel's
+all-features build next to the per-scene feature variants the host picks (RRTE_GENERIC_ALL), with and
+without the one-leaf march dispatch and the short-program fast paths (RRTE_SDF_LEAF_DISPATCH,
+RRTE_SDF_FASTPATH are build switches of the library: their A/B builds are tools/generic_ab.sh's)."""
 import pytest
 
 import scenes_extra as se
-from rrte_amd import AmbientLight, Raytracer, scenes
+from rrte_amd import AmbientLight, scenes
 from rrte_amd import abi
 from test_gpu_parity import compare
 
@@ -15,8 +15,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _ambient_showcase(w, h, mode="lambert_shadow"):
-    """sdf-showcase with an ambient light between its point lights (the repacked shading adds every
-    light's term in light order, ambient included)."""
+    """sdf-showcase with an ambient light between its point lights."""
     objs, lights, cam, cfg = scenes.sdf_showcase(w, h, mode=mode)
     lights.insert(1, AmbientLight.default_ambient())
     return objs, lights, cam, cfg
@@ -25,39 +24,20 @@ def _ambient_showcase(w, h, mode="lambert_shadow"):
 CASES = {
     "sdf-showcase": lambda: scenes.sdf_showcase(320, 180),
     "sdf-showcase-1080p": lambda: scenes.sdf_showcase(1920, 1080),
-    "advanced-demo": lambda: scenes.advanced_demo(320, 180),      # 5 point lights: up to 5 rounds
+    "advanced-demo": lambda: scenes.advanced_demo(320, 180),      # 5 point lights
     "basic-demo": lambda: scenes.basic_demo(320, 240, mode="lambert_shadow"),
-    "ambient": lambda: _ambient_showcase(320, 180),
+    "ambient": lambda: _ambient_showcase(320, 180),  # an ambient light between point lights
     "deformers": lambda: se.deformers_scene(200, 120, "lambert_shadow"),
     "cull-stress": lambda: se.cull_stress_scene(240, 160, "lambert_shadow", n_spheres=40),
-    "all-lights": lambda: se.all_lights_scene(200, 120, "lambert_shadow"),  # (not repacked: spot, directional)
+    "all-lights": lambda: se.all_lights_scene(200, 120, "lambert_shadow"),  # point, directional, spot, ambient
 }
 
 
 @pytest.mark.parametrize("case", sorted(CASES))
-@pytest.mark.parametrize("opt", ["-DRRTE_SHADOW_REPACK=1", "-DRRTE_SQRT_BRANCHFREE"])
+@pytest.mark.parametrize("opt", ["-DRRTE_SQRT_BRANCHFREE"])
 def test_specialised_kernel_variant_matches_oracle(case, opt, monkeypatch):
     monkeypatch.setenv("RRTE_JIT_EXTRA_OPTS", opt)
     compare(*CASES[case](), linear_exact=case != "all-lights", jit=abi.JIT_ON)
-
-
-@pytest.mark.parametrize("case", ["sdf-showcase", "advanced-demo", "ambient"])
-def test_shadow_repack_equals_plain_loop(case, monkeypatch):
-    """Bit for bit against the plain shading loop on the same specialised kernel path, culling on and
-    off (the repacked rounds test under the union of their lights' cull masks)."""
-    objs, lights, cam, cfg = CASES[case]()
-    out = {}
-    for cull in ("0", "1"):
-        monkeypatch.setenv("RRTE_CULL", cull)
-        for opt in ("", "-DRRTE_SHADOW_REPACK=1"):
-            monkeypatch.setenv("RRTE_JIT_EXTRA_OPTS", opt)
-            rt = Raytracer(cfg, device=0, jit=abi.JIT_ON)
-            _, lin = rt.render_f32(objs, lights, [], cam, linear=True)
-            out[(cull, opt)] = (lin.view(np.uint32).copy(), int(rt.stats().shadow_rays))
-    ref = out[("1", "")]
-    for k, v in out.items():
-        assert np.array_equal(v[0], ref[0]), k
-        assert v[1] == ref[1], k
 
 
 @pytest.mark.parametrize("name,mode", [("sdf-showcase", "lambert_shadow"), ("basic-demo", "refcompat"),
