@@ -37,7 +37,9 @@ CASES = {
 @pytest.mark.parametrize("opt", ["-DRRTE_SQRT_BRANCHFREE"])
 def test_specialised_kernel_variant_matches_oracle(case, opt, monkeypatch):
     monkeypatch.setenv("RRTE_JIT_EXTRA_OPTS", opt)
-    compare(*CASES[case](), linear_exact=case != "all-lights", jit=abi.JIT_ON)
+    # (spot lights use acosf -- libm against the device's ocml: an ulp in the linear image, as in
+    # test_gpu_parity.py's culling tests)
+    compare(*CASES[case](), linear_exact=case not in ("all-lights", "cull-stress"), jit=abi.JIT_ON)
 
 
 @pytest.mark.parametrize("name,mode", [("sdf-showcase", "lambert_shadow"), ("basic-demo", "refcompat"),
