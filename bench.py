@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stock", action="store_true", help="skip the stock-config secondary measurement")
+    ap.add_argument("--no-boundary", action="store_true",
+                    help="skip the blocking drop-in measurement (profiles: only the headline's launches in the trace)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: consecutive frames rotate over this many streams + output buffers "
                          "so one frame's tail overlaps the next frame's start (1 = strictly one after another); "
@@ -539,7 +541,7 @@ def main():
     # into a fresh zeroed buffer per frame as the reference allocates one (`vec![0u8; w*h*4]`,
     # raytracer.rs:54).  Not the headline (SURVEY §8d excludes D2H); rank 0, N = 1 only.
     boundary = None
-    if world == 1:
+    if world == 1 and not args.no_boundary:
         hbuf = np.zeros(W * H * 4, dtype=np.uint8)
         pout = lambda b: b.ctypes.data_as(C.POINTER(C.c_uint8))  # noqa: E731
         for _ in range(3):

@@ -20,11 +20,11 @@ for k in $(seq 1 $ROUNDS); do
     name=${spec%%|*}; envs=${spec#*|}
     d=$OUT/${name}_r$k; mkdir -p $d
     for steps in 200 20; do
-      env $envs timeout -k 10 180 python3 $R/bench.py --no-cpu --no-stock --steps $steps > $d/bench$steps.log 2>&1 \
+      env $envs timeout -k 10 180 python3 $R/bench.py --no-cpu --no-stock --no-boundary --steps $steps > $d/bench$steps.log 2>&1 \
         || { tail $d/bench$steps.log; echo "bench failed: $name"; exit 1; }
     done
     # (the program itself right after --: env assignments are exported before rocprofv3 starts)
-    ( [ -n "$envs" ] && export $envs; timeout -s KILL 120 rocprofv3 --pmc $COUNTERS --output-format csv -d $d/pmc -o run -- python3 $R/bench.py --no-cpu --no-stock --steps 20 > $d/pmc.log 2>&1 ) \
+    ( [ -n "$envs" ] && export $envs; timeout -s KILL 120 rocprofv3 --pmc $COUNTERS --output-format csv -d $d/pmc -o run -- python3 $R/bench.py --no-cpu --no-stock --no-boundary --steps 20 > $d/pmc.log 2>&1 ) \
       || { tail $d/pmc.log; echo "pmc failed: $name"; exit 1; }
     python3 - "$d" "$name" "$k" <<'PY'
 import csv, json, sys, collections
