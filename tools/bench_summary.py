@@ -11,5 +11,6 @@ out = {"value": d["value"], "ms_per_step": d["ms_per_step"], "avg_launch_ms": r.
        "boundary": (d.get("boundary") or {}).get("ms_per_frame_reused_buffer"),
        "hot": d.get("tile_order", {}).get("hot_slots")}
 if "kernel_kinds" in d:
-    out["kinds"] = {k: v["ms_per_frame"] for k, v in d["kernel_kinds"].items() if isinstance(v, dict)}
+    out["kinds"] = {k: v.get("ms_per_frame", v.get("generic_ms_per_frame")) for k, v in d["kernel_kinds"].items()
+                    if isinstance(v, dict)}
 print(json.dumps(out))
