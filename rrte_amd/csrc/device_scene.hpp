@@ -163,10 +163,6 @@ struct KParams {
     // tiles of every frame path; 5: 32x2, each wave storing two whole 128-B lines of RGBA8 -- the
     // blocking path's zero-copy stores into pinned host memory cross PCIe as full lines)
     uint32_t tile_shift;
-    // Slots [slot0, slot_end) of the list (KParams::hot) this launch renders: slot k = slot0 + blockIdx.z *
-    // tiles_x + blockIdx.x.  A whole list by default; a batch's launch may run its head -- the slowest
-    // tiles -- as a launch of its own on a high-priority stream (rrte_hip.hip issue_launch)
-    uint32_t slot0, slot_end;
     // Output rows: 0 = this launch's rows packed (row r at r * width, frame z at out + z * frame_stride),
     // 1 = at their image rows of frame z's own buffer cam[z].out (image_row(r) * width: a multi-GPU
     // root renders its own bands straight into the final frames; RGBA8 only)

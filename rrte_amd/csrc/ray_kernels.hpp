@@ -2090,8 +2090,8 @@ __device__ __forceinline__ LaunchTile launch_tile(const KParams& kp) {
     if (!kWg64) return LaunchTile{blockIdx.x, blockIdx.y, blockIdx.z, true};
     LaunchTile t{blockIdx.x, blockIdx.z, blockIdx.y, true};
     if (kp.hot) {
-        const uint32_t k = kp.slot0 + blockIdx.z * kp.tiles_x + blockIdx.x;
-        t.run = k < kp.slot_end;
+        const uint32_t k = blockIdx.z * kp.tiles_x + blockIdx.x;
+        t.run = k < kp.hot_n;
         const uint32_t h = kp.hot[t.run ? (k & 7u) * kp.hot_stride + (k >> 3) : 0u];
         t.x = hot_x(h);
         t.y = hot_y(h);

@@ -220,11 +220,6 @@ struct rrte_ctx {
     // for rank shares (a launch of 1/N of a frame lasts as long as its slowest tile, so
     // per-frame launches are tail-bound; 8 frames per launch overlap their tails)
     bool env_batch_launch = true;
-    // RRTE_SPLIT_HEAD=P (per mille, 0 = off): a batch's multi-frame launch runs the first P/1000 of its
-    // tile list's slot rows (its slowest tiles) as a launch of its own on a high-priority stream
-    uint32_t env_split_head = 0;
-    hipStream_t head_stream[kBatchSlabs] = {};
-    hipEvent_t ev_split_in = nullptr, ev_split_out = nullptr;
     // Blocking drop-in path into PINNED host memory (hipHostMalloc'd by the caller, or registered with
     // rrte_hip_host_register): the kernel stores the frame straight into the caller's buffer over PCIe
     // while it renders, instead of a render followed by one 8.3 MB D2H copy.  RRTE_BND_ZEROCOPY=0 turns
@@ -1507,7 +1502,6 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     k.hot = nullptr;
     k.hot_n = 0;
     k.hot_stride = 0;
-    k.slot0 = k.slot_end = 0;
     k.tile_cost = nullptr;
     // (RRTE_DEBUG bit 5 runs one workgroup in image-order numbering: no tile order; bit 4's per-wave
     // stamps work with it)
@@ -1573,7 +1567,6 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         k.hot = tp.d_list[tp.cur];
         k.hot_n = (uint32_t)tp.slots.size();
         k.hot_stride = hot_stride(k.hot_n);
-        k.slot_end = k.hot_n;
         tp.ret[tp.cur].use(st);
     }
     if (!profile) return false;
@@ -1622,8 +1615,7 @@ void launch_generic(uint32_t need, dim3 grid, dim3 block, hipStream_t st, const 
 }
 
 // Launch plan `L` (L.k.nframes frames) on `st`; the cached scene is the plan's.
-rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d_f32, hipStream_t st,
-                         hipStream_t head_stream = nullptr) {
+rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     if (L.gy == 0) return RRTE_OK;
     Cull cl{L.cull ? c->d_bounds : nullptr, L.num_prims};
     JitKernel* jk = jit_kernel_for(c, L.mode, L.cull, L.single);
@@ -1640,65 +1632,36 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         B.ret.use(st);
     }
     c->launched.use(st);
-    const dim3 block(kBlockThreads);
-    // one kernel launch of `kk` over `gz` slot rows on `s`
-    auto go = [&](KParams& kk, uint32_t gz, hipStream_t s) -> rrte_status {
-        const dim3 grid(L.gx, kk.nframes, gz);
-        trace_rec(c, profile ? "launch ray (profiled)" : "launch ray", s, nullptr, kk.nframes, kk.rows);
-        if (jk) {
-            unsigned long long* ctr = c->d_counters;
-            MeshView mv = c->mesh_view;
-            SceneValues vals{c->d_prims, c->d_mats, c->d_lights, c->d_nodes};  // read by topology kernels
-            void* args[] = {&kk, &cl, &mv, &d_rgba, &d_f32, &ctr, &vals};
-            HostSection hs(c);
-            if (c->env_wg256)
-                HIPCHK(c, hipModuleLaunchKernel(jk->fn, (kk.width + 15) / 16, (kk.rows + 15) / 16, kk.nframes, 256, 1, 1,
-                                                0, s, args, nullptr));
-            else
-                HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, s, args, nullptr));
-            hs.lap(8);
-            return RRTE_OK;
-        }
-        SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
-                     c->mesh_view};
-        const uint32_t need = c->env_generic_all ? kFeatAll : c->scene_feat;
-        if (L.mode == RRTE_MODE_REFCOMPAT)
-            launch_generic<RRTE_MODE_REFCOMPAT, false, 0u, kFeatAnalytic, kFeatSdf>(need, grid, block, s, kk, sv, cl,
-                                                                                 d_rgba, d_f32, c->d_counters);
-        else if (L.cull)
-            launch_generic<RRTE_MODE_LAMBERT_SHADOW, true, kFeatSdf, kFeatSdf | kFeatDeform, kFeatSdf | kFeatAnalytic>(
-                need, grid, block, s, kk, sv, cl, d_rgba, d_f32, c->d_counters);
+    const dim3 grid(L.gx, L.k.nframes, L.gy), block(kBlockThreads);
+    trace_rec(c, profile ? "launch ray (profiled)" : "launch ray", st, nullptr, L.k.nframes, L.k.rows);
+    if (jk) {
+        unsigned long long* ctr = c->d_counters;
+        MeshView mv = c->mesh_view;
+        SceneValues vals{c->d_prims, c->d_mats, c->d_lights, c->d_nodes};  // read by topology kernels
+        void* args[] = {&L.k, &cl, &mv, &d_rgba, &d_f32, &ctr, &vals};
+        HostSection hs(c);
+        if (c->env_wg256)
+            HIPCHK(c, hipModuleLaunchKernel(jk->fn, (L.k.width + 15) / 16, (L.k.rows + 15) / 16, L.k.nframes, 256, 1, 1,
+                                            0, st, args, nullptr));
         else
-            launch_generic<RRTE_MODE_LAMBERT_SHADOW, false, 0u, kFeatAnalytic, kFeatSdf>(need, grid, block, s, kk, sv, cl,
-                                                                                        d_rgba, d_f32, c->d_counters);
-        HIPCHK(c, hipGetLastError());
-        return RRTE_OK;
-    };
-    // The head of the tile list -- the slowest tiles of every frame of the launch -- as a launch of its
-    // own on a high-priority stream (RRTE_SPLIT_HEAD): a later batch's slowest tiles are then dispatched
-    // as soon as they are launched instead of after every workgroup of the launches queued before it.
-    // Both parts follow everything queued on `st` and `st` continues after both.
-    const uint32_t head_rows = head_stream && L.k.hot && !profile && L.gy > 1
-                                   ? std::min(L.gy - 1u, std::max(1u, (L.gy * c->env_split_head + 999u) / 1000u))
-                                   : 0u;
-    rrte_status r;
-    if (head_rows) {
-        HIPCHK(c, ev_record(c, c->ev_split_in, st, "record split in"));
-        HIPCHK(c, ev_wait(c, head_stream, c->ev_split_in, "head waits split in"));
-        KParams kh = L.k;
-        kh.slot_end = std::min(kh.hot_n, head_rows * L.gx);
-        if ((r = go(kh, head_rows, head_stream)) != RRTE_OK) return r;
-        HIPCHK(c, ev_record(c, c->ev_split_out, head_stream, "record split out"));
-        KParams kt = L.k;
-        kt.slot0 = head_rows * L.gx;
-        if ((r = go(kt, L.gy - head_rows, st)) != RRTE_OK) return r;
-        HIPCHK(c, ev_wait(c, st, c->ev_split_out, "tail stream waits head"));
-        if (c->sb_cur >= 0) c->sb[c->sb_cur].ret.use(head_stream);
-        c->tprof[L.prof].ret[c->tprof[L.prof].cur].use(head_stream);
-        c->launched.use(head_stream);
-    } else if ((r = go(L.k, L.gy, st)) != RRTE_OK) {
-        return r;
+            HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, st, args, nullptr));
+        hs.lap(8);
+        return finish_tile_order(c, L, profile, st);
     }
+    SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
+                 c->mesh_view};
+    const KParams& k = L.k;
+    const uint32_t need = c->env_generic_all ? kFeatAll : c->scene_feat;
+    if (L.mode == RRTE_MODE_REFCOMPAT)
+        launch_generic<RRTE_MODE_REFCOMPAT, false, 0u, kFeatAnalytic, kFeatSdf>(need, grid, block, st, k, sv, cl, d_rgba,
+                                                                             d_f32, c->d_counters);
+    else if (L.cull)
+        launch_generic<RRTE_MODE_LAMBERT_SHADOW, true, kFeatSdf, kFeatSdf | kFeatDeform, kFeatSdf | kFeatAnalytic>(
+            need, grid, block, st, k, sv, cl, d_rgba, d_f32, c->d_counters);
+    else
+        launch_generic<RRTE_MODE_LAMBERT_SHADOW, false, 0u, kFeatAnalytic, kFeatSdf>(need, grid, block, st, k, sv, cl,
+                                                                                    d_rgba, d_f32, c->d_counters);
+    HIPCHK(c, hipGetLastError());
     return finish_tile_order(c, L, profile, st);
 }
 
@@ -1898,7 +1861,6 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
     if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] != '0';
-    if (const char* g = getenv("RRTE_SPLIT_HEAD")) c->env_split_head = std::min(999u, (uint32_t)strtoul(g, nullptr, 0));
     if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
     if (const char* g = getenv("RRTE_ZC_TILE_SHIFT"))
         c->zc_tile_shift = std::max(3u, std::min(5u, (uint32_t)strtoul(g, nullptr, 0)));
@@ -2016,8 +1978,6 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_batch)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {c->ev_split_in, c->ev_split_out})
-        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_render)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->batch.ev_src)
@@ -2026,7 +1986,6 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (c->d_bsend[i]) (void)hipFree(c->d_bsend[i]);
         if (c->d_brecv[i]) (void)hipFree(c->d_brecv[i]);
         if (c->render_stream[i]) (void)hipStreamDestroy(c->render_stream[i]);
-        if (c->head_stream[i]) (void)hipStreamDestroy(c->head_stream[i]);
     }
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2439,7 +2398,7 @@ static rrte_status render_batch(rrte_ctx* c, bool at_flush) {
         L.k.frame_stride = b.slice;
         L.k.out_image_rows = b.in_place ? 1u : 0u;
         uint8_t* dst = b.in_place ? nullptr : base + (size_t)j0 * b.slice;
-        rrte_status r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, rs, c->head_stream[k]);
+        rrte_status r = issue_launch(c, L, reinterpret_cast<uint32_t*>(dst), nullptr, rs);
         if (r != RRTE_OK) return r;
     }
     b.rendered = b.n;
@@ -2700,12 +2659,6 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             int lo = 0, hi = 0;
             HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
             HIPCHK(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, c->env_comm_priority ? hi : lo));
-            for (int i = 0; i < c->batch_slabs && c->env_split_head; ++i)
-                HIPCHK(c, hipStreamCreateWithPriority(&c->head_stream[i], hipStreamNonBlocking, hi));
-            if (c->env_split_head) {
-                HIPCHK(c, hipEventCreateWithFlags(&c->ev_split_in, hipEventDisableTiming));
-                HIPCHK(c, hipEventCreateWithFlags(&c->ev_split_out, hipEventDisableTiming));
-            }
             for (int i = 0; i < c->batch_slabs; ++i) {  // (only the slots of the ring in use)
                 HIPCHK(c, hipStreamCreateWithFlags(&c->render_stream[i], hipStreamNonBlocking));
                 HIPCHK(c, hipEventCreateWithFlags(&c->ev_batch[i], hipEventDisableTiming));
@@ -2715,7 +2668,6 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
             // its first dispatch, which must not happen inside a later frame's critical path
             for (int i = 0; i < c->batch_slabs; ++i) {
                 hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, c->render_stream[i]);
-                if (c->head_stream[i]) hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, c->head_stream[i]);
                 HIPCHK(c, hipGetLastError());
             }
             hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, c->comm_stream);

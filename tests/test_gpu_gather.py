@@ -63,18 +63,6 @@ def test_multi_frame_batch_launches(batch, route, monkeypatch):
     _check_gather(False, abi.JIT_ON, batch, monkeypatch, None)
 
 
-@pytest.mark.parametrize("route", ["in_place", "self"])
-def test_split_head_launches(route, monkeypatch):
-    """RRTE_SPLIT_HEAD: a batch's multi-frame launch runs the head of its tile list (here a fixed
-    permutation, RRTE_TILE_ORDER=2, so every launch has one) as a launch of its own on a high-priority
-    stream and the rest on the render stream; every frame is still exact."""
-    monkeypatch.setenv("RRTE_SPLIT_HEAD", "250")
-    monkeypatch.setenv("RRTE_TILE_ORDER", "2")
-    if route == "self":
-        monkeypatch.setenv("RRTE_GATHER_SELF", "1")
-    _check_gather(False, abi.JIT_ON, 8, monkeypatch, None)
-
-
 @pytest.mark.parametrize("alpha,rgb24", [(None, "0"), ("material", "1"), ("spp2", "1")])
 def test_gather_slab_formats(alpha, rgb24, monkeypatch):
     """RGBA8 slabs when forced (RRTE_GATHER_RGB24=0) or when some alpha byte is not 255; every
