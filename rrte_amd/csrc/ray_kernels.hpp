@@ -657,9 +657,6 @@ __device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float
 #ifndef RRTE_MARCH_PRED
 #define RRTE_MARCH_PRED 0
 #endif
-#ifndef RRTE_MARCH_BITWISE
-#define RRTE_MARCH_BITWISE 0  // march exit conditions as lane-mask ops instead of short-circuit branches (A/B)
-#endif
 #define RRTE_PRAGMA_(x) _Pragma(#x)
 #define RRTE_UNROLL_(n) RRTE_PRAGMA_(unroll n)
 // One SDF evaluation with deferred guards: the short sequences for every lane, one wave-uniform test
@@ -790,15 +787,8 @@ RRTE_UNROLL_(RRTE_MARCH_UNROLL)
             float d = eval_deferred(eval, p);
             hit = d < eps * t;
             const float tn = t + d * scale;
-#if RRTE_MARCH_BITWISE
-            // every condition evaluated (no side effects), combined as lane masks: one divergent exit
-            // per step instead of the nested exec save / restore chains short-circuit evaluation makes
-            const bool safe = (d - E * t >= D3) & ((d - dp) - E * (t - tp) >= D3);
-            const bool stop = hit | (tn > tend) | safe;
-#else
             const bool safe = (d - E * t >= D3) && ((d - dp) - E * (t - tp) >= D3);
             const bool stop = hit || tn > tend || safe;
-#endif
             dp = d;
             tp = t;
             t = hit ? t : tn;
@@ -813,11 +803,7 @@ RRTE_UNROLL_(RRTE_MARCH_UNROLL)
         float d = eval_deferred(eval, p);
         hit = d < eps * t;
         const float tn = t + d * scale;
-#if RRTE_MARCH_BITWISE
-        const bool stop = hit | (tn > tend);
-#else
         const bool stop = hit || tn > tend;
-#endif
         t = hit ? t : tn;
         if (stop) break;
     }
