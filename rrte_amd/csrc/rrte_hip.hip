@@ -229,7 +229,14 @@ struct rrte_ctx {
     uint32_t zc_tile_shift = 5;       // ... of zero-copy blocking frames (RRTE_ZC_TILE_SHIFT: 3 / 4 / 5)
     struct HostReg { void* p; size_t bytes; };
     std::vector<HostReg> host_regs;   // rrte_hip_host_register'ed ranges (unregistered at destroy)
-    struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, valid; JitKernel* k; } jit_last{};
+    struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, uniform, valid; JitKernel* k; } jit_last{};
+    // Guard flavour of the scene-specialised kernel (device_scene.hpp RRTE_GUARD_UNIFORM): the correctly
+    // rounded sequences' rare fallbacks as wave-uniform branches on a ballot (fewer scalar-unit
+    // instructions, a longer dependent chain) for frames that stream -- the async and gather entry
+    // points -- and as divergent branches for the blocking single frame, which is latency-bound
+    // (measured, DESIGN.md §13: streams -1.8 %, a lone frame +12 %).  RRTE_GUARD_POLICY=0/1 forces one.
+    bool jit_stream = true;         // the current call streams frames (false inside rrte_hip_render)
+    int env_guard_policy = -1;
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
     // topology kernels (jit.hip JitTopo): the cached scene's topology key and structural decisions, and
     // how many consecutive scene changes kept that topology (value edits: an animation)
@@ -1221,18 +1228,21 @@ bool jit_wants_topology(const rrte_ctx* c) {
            (c->env_jit_topo == 2 && c->value_edits >= 1 && c->same_scene_renders < kJitFullAfter);
 }
 
-std::string jit_key(const rrte_ctx* c, bool topo, int mode, bool cull, bool single) {
+std::string jit_key(const rrte_ctx* c, bool topo, int mode, bool cull, bool single, bool uniform) {
     std::string key(1, topo ? 'T' : 'F');
     if (topo) key += c->topo_key;
     else key.append(c->scene_key.begin(), c->scene_key.end());
     key.push_back((char)mode);
     key.push_back((char)cull);
     key.push_back((char)single);
+    key.push_back((char)uniform);
     return key;
 }
 
+bool jit_uniform_guards(const rrte_ctx* c) { return c->env_guard_policy >= 0 ? c->env_guard_policy != 0 : c->jit_stream; }
+
 // The cached kernel for `key`, compiling it if the JIT policy says so; nullptr = not available (yet).
-JitKernel* jit_lookup(rrte_ctx* c, const std::string& key, bool topo, int mode, bool cull, bool single) {
+JitKernel* jit_lookup(rrte_ctx* c, const std::string& key, bool topo, int mode, bool cull, bool single, bool uniform) {
     auto it = c->jit_cache.find(key);
     if (it != c->jit_cache.end()) return it->second.fn ? &it->second : nullptr;
     JitKernel jk;
@@ -1267,6 +1277,7 @@ JitKernel* jit_lookup(rrte_ctx* c, const std::string& key, bool topo, int mode, 
                                      c->h_nodes.data(), (uint32_t)c->h_nodes.size(), mode, cull, single,
                                      topo ? &c->topo : nullptr);
         if (c->env_wg256) src = "#define RRTE_WG256 1\n" + src;
+        if (uniform) src = "#define RRTE_GUARD_UNIFORM 1\n" + src;
         if (c->jit_mode == RRTE_JIT_AUTO) {
             // compile on a background thread (hiprtc only); frames keep running on the current kernel
             c->jit_pending.emplace(key, std::async(std::launch::async, [src]() { return jit_compile_code(src); }));
@@ -1289,17 +1300,18 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
     if (c->jit_mode == RRTE_JIT_OFF) return nullptr;
     auto& last = c->jit_last;  // per-frame fast path: same scene, mode, policy and kernel kind as the last frame
     const bool topo = jit_wants_topology(c);
+    const bool uniform = jit_uniform_guards(c);
     if (last.valid && last.gen == c->scene_gen && last.mode == mode && last.cull == cull && last.single == single &&
-        last.jit_mode == c->jit_mode && last.topo == topo)
+        last.jit_mode == c->jit_mode && last.topo == topo && last.uniform == uniform)
         return last.k;
     if (c->h_prims.size() > kJitMaxPrims || c->h_nodes.size() > kJitMaxNodes) return nullptr;
-    const std::string key = jit_key(c, topo, mode, cull, single);
-    JitKernel* k = jit_lookup(c, key, topo, mode, cull, single);
+    const std::string key = jit_key(c, topo, mode, cull, single, uniform);
+    JitKernel* k = jit_lookup(c, key, topo, mode, cull, single, uniform);
     if (!k && !c->jit_cache.count(key)) {
         // not available yet (AUTO: not due, or compiling in the background): not remembered, asked again
         // next frame.  The full kernel of a scene that stopped changing: its topology kernel meanwhile
         if (!topo && c->env_jit_topo == 2 && c->value_edits >= 1) {
-            auto it = c->jit_cache.find(jit_key(c, true, mode, cull, single));
+            auto it = c->jit_cache.find(jit_key(c, true, mode, cull, single, uniform));
             if (it != c->jit_cache.end() && it->second.fn) return &it->second;
         }
         return nullptr;
@@ -1310,6 +1322,7 @@ JitKernel* jit_kernel_for(rrte_ctx* c, int mode, bool cull, bool single) {
     last.cull = cull;
     last.single = single;
     last.topo = topo;
+    last.uniform = uniform;
     last.k = k;
     last.valid = true;
     return k;
@@ -1765,6 +1778,7 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     const int nr = c->nranks, rk = c->rank;
     c->nranks = 1;
     c->rank = 0;
+    c->jit_stream = false;  // (one blocking frame: the latency flavour of the specialised kernel)
     // pinned caller buffer: the kernel writes the frame into it directly (no D2H copy afterwards)
     uint32_t* zc = out8 && !outf && c->env_bnd_zerocopy ? pinned_device_ptr(out8, npix * 4) : nullptr;
     const bool chunked = !zc && out8 && !outf && c->bnd_chunks > 1 && p->height >= 32u && !c->env_debug;
@@ -1779,6 +1793,7 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     }
     c->nranks = nr;
     c->rank = rk;
+    c->jit_stream = true;
     if (r != RRTE_OK) return r;
     c->pending_kernel_timing = true;
     c->pending_primary = (uint64_t)npix * p->samples_per_pixel;
@@ -1860,6 +1875,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_COMM_PRIORITY")) c->env_comm_priority = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
+    if (const char* g = getenv("RRTE_GUARD_POLICY"); g && *g) c->env_guard_policy = g[0] != '0' ? 1 : 0;
     if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] != '0';
     if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
     if (const char* g = getenv("RRTE_ZC_TILE_SHIFT"))

@@ -50,3 +50,12 @@ def test_generic_all_features_build(name, mode, monkeypatch):
     for flag in ("1", "0"):
         monkeypatch.setenv("RRTE_GENERIC_ALL", flag)
         compare(*scenes.SCENES[name](200, 120, mode=mode), jit=abi.JIT_OFF)
+
+
+@pytest.mark.parametrize("case", ["sdf-showcase", "deformers", "advanced-demo", "cull-stress"])
+@pytest.mark.parametrize("policy", ["0", "1"])
+def test_guard_flavours_match_oracle(case, policy, monkeypatch):
+    """Both guard flavours of the specialised kernel (RRTE_GUARD_POLICY=1: wave-uniform fallback
+    branches, the streaming entry points' default; 0: divergent, the blocking frame's) are exact."""
+    monkeypatch.setenv("RRTE_GUARD_POLICY", policy)
+    compare(*CASES[case](), linear_exact=case != "cull-stress", jit=abi.JIT_ON)
