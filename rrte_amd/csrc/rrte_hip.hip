@@ -232,11 +232,12 @@ struct rrte_ctx {
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, uniform, valid; JitKernel* k; } jit_last{};
     // Guard flavour of the scene-specialised kernel (device_scene.hpp RRTE_GUARD_UNIFORM): the correctly
     // rounded sequences' rare fallbacks as wave-uniform branches on a ballot (fewer scalar-unit
-    // instructions, a longer dependent chain) for frames that stream -- the async and gather entry
-    // points -- and as divergent branches for the blocking single frame, which is latency-bound
-    // (measured, DESIGN.md §13: streams -1.8 %, a lone frame +12 %).  RRTE_GUARD_POLICY=0/1 forces one.
+    // instructions, a longer dependent chain) or as divergent branches (measured, DESIGN.md §13: frame
+    // streams -1.8 %, a lone frame +12 %).  RRTE_GUARD_POLICY: 0 divergent everywhere (default), 1
+    // uniform everywhere, 2 uniform for the streaming entry points (async, gather) and divergent for
+    // the blocking frame.
     bool jit_stream = true;         // the current call streams frames (false inside rrte_hip_render)
-    int env_guard_policy = -1;
+    int env_guard_policy = 0;
     uint64_t same_scene_renders = 0;             // consecutive renders of the cached scene
     // topology kernels (jit.hip JitTopo): the cached scene's topology key and structural decisions, and
     // how many consecutive scene changes kept that topology (value edits: an animation)
@@ -1239,7 +1240,7 @@ std::string jit_key(const rrte_ctx* c, bool topo, int mode, bool cull, bool sing
     return key;
 }
 
-bool jit_uniform_guards(const rrte_ctx* c) { return c->env_guard_policy >= 0 ? c->env_guard_policy != 0 : c->jit_stream; }
+bool jit_uniform_guards(const rrte_ctx* c) { return c->env_guard_policy == 2 ? c->jit_stream : c->env_guard_policy == 1; }
 
 // The cached kernel for `key`, compiling it if the JIT policy says so; nullptr = not available (yet).
 JitKernel* jit_lookup(rrte_ctx* c, const std::string& key, bool topo, int mode, bool cull, bool single, bool uniform) {
@@ -1875,7 +1876,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_COMM_PRIORITY")) c->env_comm_priority = g[0] != '0';
     if (const char* g = getenv("RRTE_WG64")) c->env_wg256 = g[0] == '0';
     if (const char* g = getenv("RRTE_GENERIC_ALL")) c->env_generic_all = g[0] == '1';
-    if (const char* g = getenv("RRTE_GUARD_POLICY"); g && *g) c->env_guard_policy = g[0] != '0' ? 1 : 0;
+    if (const char* g = getenv("RRTE_GUARD_POLICY"); g && *g) c->env_guard_policy = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] != '0';
     if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
     if (const char* g = getenv("RRTE_ZC_TILE_SHIFT"))
