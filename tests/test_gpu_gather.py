@@ -54,10 +54,11 @@ def test_gather_path_matches_plain_render(overlap, jit, batch, route, monkeypatc
 
 @pytest.mark.parametrize("route", ["in_place", "self"])
 @pytest.mark.parametrize("batch", [3, 8])
-def test_multi_frame_batch_launches(batch, route, monkeypatch):
-    """RRTE_BATCH_LAUNCH=1: a batch's frames rendered together in multi-frame launches at its close
-    (round 4's policy, kept as an A/B switch) instead of one launch per frame at its call."""
-    monkeypatch.setenv("RRTE_BATCH_LAUNCH", "1")
+def test_per_frame_batch_launches(batch, route, monkeypatch):
+    """RRTE_BATCH_LAUNCH=0: each frame of a batch launched at its call on its caller's stream (the
+    root in place, a peer into its send-slab slot) with only the exchange batched -- an A/B policy
+    (measured slower than the default multi-frame launches)."""
+    monkeypatch.setenv("RRTE_BATCH_LAUNCH", "0")
     if route == "self":
         monkeypatch.setenv("RRTE_GATHER_SELF", "1")
     _check_gather(False, abi.JIT_ON, batch, monkeypatch, None)
