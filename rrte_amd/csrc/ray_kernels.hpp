@@ -657,6 +657,9 @@ __device__ __forceinline__ bool leaves_sphere(float hb, float cc, float a, float
 #ifndef RRTE_MARCH_PRED
 #define RRTE_MARCH_PRED 0
 #endif
+#ifndef RRTE_MARCH_PAIR
+#define RRTE_MARCH_PAIR 0  // sphere-tracing loops exit every second step (A/B)
+#endif
 #define RRTE_PRAGMA_(x) _Pragma(#x)
 #define RRTE_UNROLL_(n) RRTE_PRAGMA_(unroll n)
 // One SDF evaluation with deferred guards: the short sequences for every lane, one wave-uniform test
@@ -781,6 +784,30 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
                          ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
                           ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
         float dp = __builtin_nanf(""), tp = t;
+#if RRTE_MARCH_PAIR
+        // two steps per loop exit (see below)
+        for (uint32_t i = 0; i < steps; i += 2u) {
+            const float dA = eval_deferred(eval, ray_at(r, t));
+            const bool hitA = dA < eps * t;
+            const float tnA = t + dA * scale;
+            const bool stopA = hitA || tnA > tend || ((dA - E * t >= D3) && ((dA - dp) - E * (t - tp) >= D3));
+            const float tA = hitA ? t : tnA;
+            if (i + 1u >= steps) {  // (uniform: an odd step cap ends on a single step)
+                hit = hitA;
+                t = tA;
+                break;
+            }
+            const float dB = eval_deferred(eval, ray_at(r, tA));
+            const bool hitB = dB < eps * tA;
+            const float tnB = tA + dB * scale;
+            const bool stopB = hitB || tnB > tend || ((dB - E * tA >= D3) && ((dB - dA) - E * (tA - t) >= D3));
+            hit = stopA ? hitA : hitB;
+            dp = stopA ? dA : dB;
+            tp = stopA ? t : tA;
+            t = stopA ? tA : (hitB ? tA : tnB);
+            if (stopA || stopB) break;
+        }
+#else
 RRTE_UNROLL_(RRTE_MARCH_UNROLL)
         for (uint32_t i = 0; i < steps; ++i) {
             f3 p = ray_at(r, t);
@@ -794,9 +821,36 @@ RRTE_UNROLL_(RRTE_MARCH_UNROLL)
             t = hit ? t : tn;
             if (stop) break;
         }
+#endif
         t_hit = t;
         return hit;
     }
+#if RRTE_MARCH_PAIR
+    // Two march steps per loop exit: the second step runs on every lane that entered the iteration,
+    // and a lane whose first step stopped keeps that step's result through selects -- the same t
+    // sequence and result per lane as one exit per step, with half the divergent-exit bookkeeping on
+    // the scalar unit (a wave whose last lanes stop on a first step pays one extra step).
+    for (uint32_t i = 0; i < steps; i += 2u) {
+        const float dA = eval_deferred(eval, ray_at(r, t));
+        const bool hitA = dA < eps * t;
+        const float tnA = t + dA * scale;
+        const bool stopA = hitA || tnA > tend;
+        const float tA = hitA ? t : tnA;
+        if (i + 1u >= steps) {
+            hit = hitA;
+            t = tA;
+            break;
+        }
+        const float dB = eval_deferred(eval, ray_at(r, tA));
+        const bool hitB = dB < eps * tA;
+        const float tnB = tA + dB * scale;
+        hit = stopA ? hitA : hitB;
+        t = stopA ? tA : (hitB ? tA : tnB);
+        if (stopA || hitB || tnB > tend) break;
+    }
+    t_hit = t;
+    return hit;
+#endif
 RRTE_UNROLL_(RRTE_MARCH_UNROLL)
     for (uint32_t i = 0; i < steps; ++i) {
         f3 p = ray_at(r, t);
