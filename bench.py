@@ -482,8 +482,12 @@ def main():
         # poll for the end of the work (events on every stream the frames and the library used)
         # before the closing synchronize: a blocking device synchronize wakes the host ~40 us after
         # the last kernel ends (tools/runs/r02_timeline2.sh); the work measured is the same
-        ends = [torch.cuda.Event() for _ in streams]
-        for e, s in zip(ends, streams):
+        # (the streams the timed frames were issued on: an event on a stream no frame used is the first
+        # work that stream ever sees, and with every frame buffer's stream over HIP's hardware-queue
+        # limit -- 16 in flight -- that first dispatch waited ~10 ms for a queue, inside the timed region)
+        used = streams[:NS] if gath else streams
+        ends = [torch.cuda.Event() for _ in used]
+        for e, s in zip(ends, used):
             e.record(s)
         busy = C.c_uint32(1)
         while busy.value or not all(e.query() for e in ends):
