@@ -1171,6 +1171,17 @@ BandMap band_layout(const rrte_camera& cam, const std::vector<float4>& bounds, u
     // keep the smaller cycle
     constexpr double kSkyCost = 0.15, kExpandCost = 0.09;
     const uint32_t nb = (height + band_rows - 1) / band_rows;
+    // The choice depends on the sky count, not on the camera itself: a moving camera repeats a few sky
+    // counts, so each (sky, frame height, band height, ranks) is searched once (the search over every
+    // pair and band was most of a moving-camera frame call's host time)
+    struct Choice { uint32_t sky, height, band_rows, nranks, a, b; };
+    thread_local std::vector<Choice> memo;
+    for (const Choice& ch : memo)
+        if (ch.sky == m.sky && ch.height == height && ch.band_rows == band_rows && ch.nranks == (uint32_t)nranks) {
+            m.root_bands = ch.a;
+            m.peer_bands = ch.b;
+            return m;
+        }
     std::vector<double> load((size_t)nranks);
     double best = std::numeric_limits<double>::infinity();
     for (uint32_t a = 0; a <= kMaxCycleBands; ++a)
@@ -1188,6 +1199,8 @@ BandMap band_layout(const rrte_camera& cam, const std::vector<float4>& bounds, u
             const double busiest = *std::max_element(load.begin(), load.end());
             if (busiest < best - 1e-9) best = busiest, m.root_bands = a, m.peer_bands = b;
         }
+    if (memo.size() >= 64) memo.clear();
+    memo.push_back(Choice{m.sky, height, band_rows, (uint32_t)nranks, m.root_bands, m.peer_bands});
     return m;
 }
 
@@ -1382,11 +1395,20 @@ const BandMap& frame_band_map(rrte_ctx* c, const rrte_scene_ir* s, const rrte_re
         bc.root = root;
         bc.rank = c->rank;
         bc.cam = s->camera;
-        bc.rows = rows_for_rank(p->height, p->band_rows, c->nranks, c->rank, bc.m.sky, bc.m.root_bands, bc.m.peer_bands);
-        bc.cap = 0;
-        for (int q = 0; q < c->nranks; ++q)
-            bc.cap = std::max(bc.cap, rows_for_rank(p->height, p->band_rows, c->nranks, q, bc.m.sky, bc.m.root_bands,
-                                                    bc.m.peer_bands));
+        // every rank's rows in one pass over the bands (as rows_for_rank counts them)
+        std::vector<uint32_t> per((size_t)c->nranks, 0u);
+        if (c->nranks <= 1 || p->band_rows == 0) {
+            per.assign((size_t)std::max(c->nranks, 1), p->height);
+        } else {
+            const uint32_t nb = (p->height + p->band_rows - 1) / p->band_rows;
+            for (uint32_t b = 0; b < nb; ++b) {
+                uint32_t lb = 0;
+                const uint32_t r0 = b * p->band_rows, r1 = std::min(r0 + p->band_rows, p->height);
+                per[band_owner(bc.m, b, lb)] += r1 - r0;
+            }
+        }
+        bc.rows = per[(size_t)c->rank];
+        bc.cap = *std::max_element(per.begin(), per.end());
     }
     if (rows) *rows = bc.rows;
     if (cap) *cap = bc.cap;
@@ -2652,10 +2674,23 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
     rrte_render_params pp = *p;
     pp.band_rows = band;
     uint32_t rows = p->height, cap = p->height;  // this rank's rows; slab rows (the most any rank owns)
-    const BandMap bm = c->nranks > 1 ? frame_band_map(c, s, &pp, root, &rows, &cap) : BandMap{band, 1u, 0u, 1u, 1u};
     const bool rgb24 = slab_rgb24(c, s, p);
+    // A frame joining an open batch of the same frame geometry keeps the batch's band partition: which
+    // rank renders a band is a work-balance choice, never a pixel, and every rank makes the same one
+    // from the same calls -- so a moving camera neither recomputes the partition every frame nor
+    // closes the batch whenever its sky-band count changes
+    const rrte_ctx::Batch& ob = c->batch;
+    const bool join = c->nranks > 1 && c->gather_batch > 1 && !timing && ob.n && ob.width == p->width &&
+                      ob.height == p->height && ob.band == band && ob.root == root && ob.rgb24 == rgb24;
+    BandMap bm{band, 1u, 0u, 1u, 1u};
+    if (join) {
+        bm = ob.bm;
+        rows = ob.plan.k.rows;
+    } else if (c->nranks > 1) {
+        bm = frame_band_map(c, s, &pp, root, &rows, &cap);
+    }
     // bytes per rank slot, 256-B aligned so every rank's send buffer starts aligned
-    const size_t slice = ((size_t)cap * p->width * (rgb24 ? 3u : 4u) + 255u) & ~(size_t)255u;
+    const size_t slice = join ? ob.slice : ((size_t)cap * p->width * (rgb24 ? 3u : 4u) + 255u) & ~(size_t)255u;
     const uint32_t kflags = rgb24 ? kFlagSlabRgb24 : 0u;
     if (c->comm_failed)
         return fail(c, RRTE_RCCL_ERROR, "communicator aborted earlier (%s); call rrte_hip_comm_init", c->comm_fail_msg.c_str());
