@@ -279,7 +279,7 @@ def auto_cold_start(scene, prm, fulls, sptrs, dev, rays_per_frame, limit_s=8.0):
                     "kernel until the background hiprtc compile lands (include/rrte_hip.h RRTE_JIT_AUTO)"}
 
 
-def kernel_variants(scene, prm, fulls, sptrs, dev, rays_per_frame, anim=None, n=60):
+def kernel_variants(scene, prm, fulls, sptrs, dev, rays_per_frame, anim=None, n=200):
     """Secondary throughput of the headline workload per kernel kind (rank 0, N=1; not the headline):
     the generic kernel, the TOPOLOGY specialisation (structure compiled in, values read from the
     uploaded scene: one compile serves every frame of an animation), the FULL specialisation (the
