@@ -1047,12 +1047,24 @@ void tile_rects(bool enabled, const std::vector<float4>& bounds, const rrte_scen
         to_cam(w, v);
         const bool finite = std::isfinite(R) && std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]);
         if (finite && R >= 0.0 && v[2] < -R * 1.001 - 1e-6) {  // entirely in front of the eye (z < 0)
-            // tangent slopes of the disc (centre (c, -d), radius R, d > R) seen from the origin
+            // tangent slopes of the disc (centre (c, -d), radius R, d > R) seen from the origin:
+            // tan(alpha -/+ beta) with tan alpha = c / d and tan beta = R / sqrt(D^2 - R^2), by the
+            // angle-sum identity (no trigonometry: this runs per object for every new camera).  The
+            // disc lies in z < 0, so both tangents point forward (|alpha +/- beta| < pi/2) and both
+            // denominators are positive; a non-positive one (rounding at the limit) leaves that
+            // side unbounded
             auto range = [&](double cc, double& lo, double& hi) {
-                const double d = -v[2], D = std::sqrt(cc * cc + d * d);
-                const double alpha = std::atan2(cc, d), beta = std::asin(std::min(1.0, R / D));
-                lo = std::tan(alpha - beta);
-                hi = std::tan(alpha + beta);
+                const double d = -v[2], h2 = cc * cc + d * d - R * R;
+                const double inf = std::numeric_limits<double>::infinity();
+                if (!(h2 > 0.0)) {
+                    lo = -inf;
+                    hi = inf;
+                    return;
+                }
+                const double ta = cc / d, tb = R / std::sqrt(h2);
+                const double dl = 1.0 + ta * tb, dh = 1.0 - ta * tb;
+                lo = dl > 0.0 ? (ta - tb) / dl : -inf;
+                hi = dh > 0.0 ? (ta + tb) / dh : inf;
             };
             double xl, xh, yl, yh;
             range(v[0], xl, xh);
