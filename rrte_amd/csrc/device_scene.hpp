@@ -176,6 +176,11 @@ static_assert(sizeof(KParams) <= 3584, "kernel arguments stay below the 4 KB ker
 // only when it has proved every pixel's alpha byte is 255 (rrte_hip.hip, slab_rgb24), and the
 // root's de-interleave puts the 255 back.
 constexpr uint32_t kFlagSlabRgb24 = 1u << 31;
+// Internal: the RGBA8 output is pinned HOST memory (the blocking entry point's zero-copy frame).  Its
+// pixel stores go out at system scope (write-through cache policy): plain stores into host memory
+// were measured to leave only at the kernel's end (tools/micro/zc_write.hip: no overlap with the
+// compute of waves still running), system-scope ones while the frame renders.
+constexpr uint32_t kFlagHostStore = 1u << 30;
 
 
 // ---------------------------------------------------------------- f32 vec3

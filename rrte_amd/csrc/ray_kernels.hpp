@@ -2259,6 +2259,8 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
                 b[0] = (uint8_t)px;
                 b[1] = (uint8_t)(px >> 8);
                 b[2] = (uint8_t)(px >> 16);
+            } else if (kp.flags & kFlagHostStore) {  // zero-copy frame: out now, not at the kernel's end
+                __hip_atomic_store(out_rgba8 + o, px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             } else {
                 out_rgba8[o] = px;
             }

@@ -116,6 +116,14 @@ struct rrte_ctx {
     unsigned long long* d_counters = nullptr;   // shadow rays, kCounterShards x kCounterStride (accumulating)
     unsigned long long* h_counters = nullptr;   // pinned copy
     unsigned long long shadow_base = 0;         // value at the start of the last frame
+    // The blocking frame returns once the frame itself is complete; its counter copy lands after that
+    // and is folded into rrte_stats when they are read (rrte_hip_stats) -- two pinned copy slots, so a
+    // frame's copy never overwrites the one of the frame before it while that is unread
+    unsigned long long* h_counters2 = nullptr;
+    hipEvent_t ev_ctr[2] = {};        // slot's copy landed
+    hipEvent_t ev_done = nullptr;     // the blocking frame complete (before its counter copy)
+    bool ctr_pending = false;         // the last frame's counts are in slot ctr_slot, not yet in stats
+    int ctr_slot = 0;
     // multi-GPU
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -226,6 +234,7 @@ struct rrte_ctx {
     // it off (A/B).  Pageable buffers keep the copy.
     bool env_bnd_zerocopy = true;
     uint32_t tile_shift = 3;          // tile shape of the launch being planned (KParams::tile_shift)
+    bool env_zc_system_store = true;  // ... their pixel stores at system scope (RRTE_ZC_SYSTEM_STORE=0: plain, A/B)
     uint32_t zc_tile_shift = 5;       // ... of zero-copy blocking frames (RRTE_ZC_TILE_SHIFT: 3 / 4 / 5)
     struct HostReg { void* p; size_t bytes; };
     std::vector<HostReg> host_regs;   // rrte_hip_host_register'ed ranges (unregistered at destroy)
@@ -1722,14 +1731,61 @@ rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params
     return issue_launch(c, L, d_rgba, d_f32, st);
 }
 
-// Read back the device counters and close the frame's statistics.
-rrte_status finish_frame(rrte_ctx* c) {
-    HIPCHK(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+unsigned long long* ctr_host(rrte_ctx* c, int slot) { return slot ? c->h_counters2 : c->h_counters; }
+unsigned long long ctr_total(rrte_ctx* c, int slot) {
+    const unsigned long long* h = ctr_host(c, slot);
     unsigned long long total = 0;
-    for (uint32_t i = 0; i < kCounterShards; ++i) total += c->h_counters[i * kCounterStride];
+    for (uint32_t i = 0; i < kCounterShards; ++i) total += h[i * kCounterStride];
+    return total;
+}
+
+// The last blocking frame's shadow-ray count into rrte_stats (waits for its counter copy).
+rrte_status resolve_counters(rrte_ctx* c) {
+    if (!c->ctr_pending) return RRTE_OK;
+    HIPCHK(c, hipEventSynchronize(c->ev_ctr[c->ctr_slot]));
+    const unsigned long long total = ctr_total(c, c->ctr_slot);
     c->stats.shadow_rays = total - c->shadow_base;
     c->shadow_base = total;
+    c->ctr_pending = false;
+    return RRTE_OK;
+}
+
+// Wait for `ev` by polling (a blocking wait wakes the host several us after the device signals):
+// at most ~2 ms of polling, then a blocking wait.
+rrte_status spin_wait(rrte_ctx* c, hipEvent_t ev) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return RRTE_OK;
+        if (e != hipErrorNotReady) HIPCHK(c, e);
+        if ((spin & 63u) == 63u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+            HIPCHK(c, hipEventSynchronize(ev));
+            return RRTE_OK;
+        }
+    }
+}
+
+// Read back the device counters and close the frame's statistics.  `deferred` (the blocking
+// single-context frame): return once the frame's work on the context's stream is complete; the
+// counter copy queued behind it is folded in by resolve_counters when the statistics are read.
+rrte_status finish_frame(rrte_ctx* c, bool deferred = false) {
+    // the slot the pending copy does not use (that copy precedes this one on the stream)
+    const int slot = c->ctr_pending ? 1 - c->ctr_slot : 0;
+    if (deferred) HIPCHK(c, hipEventRecord(c->ev_done, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ctr_host(c, slot), c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_ctr[slot], c->stream));
+    rrte_status r = deferred ? spin_wait(c, c->ev_done) : RRTE_OK;
+    if (r != RRTE_OK) return r;
+    if (!deferred) HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->ctr_pending) {
+        // (complete: it precedes this frame on the stream) the previous frame's counts, never read,
+        // become the base of this one's
+        c->shadow_base = ctr_total(c, c->ctr_slot);
+        c->ctr_pending = false;
+    }
+    c->ctr_slot = slot;
+    c->ctr_pending = true;
+    if (!deferred && (r = resolve_counters(c)) != RRTE_OK) return r;
     if (c->pending_kernel_timing) {
         float ms = 0.0f;
         if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->stats.kernel_ms = ms;
@@ -1822,7 +1878,8 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     } else {
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
         if (zc) c->tile_shift = c->zc_tile_shift;  // whole 128-B lines per wave across PCIe
-        r = launch(c, s, p, p->height, zc ? zc : c->d_rgba, outf ? c->d_f32 : nullptr, c->stream);
+        r = launch(c, s, p, p->height, zc ? zc : c->d_rgba, outf ? c->d_f32 : nullptr, c->stream,
+                   zc && c->env_zc_system_store ? kFlagHostStore : 0u);
         c->tile_shift = 3;
         if (r == RRTE_OK) r = hipEventRecord(c->ev1, c->stream) == hipSuccess ? RRTE_OK : RRTE_HIP_ERROR;
     }
@@ -1836,7 +1893,7 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     c->stats.gather_ms = 0.0;
     if (out8 && !chunked && !zc) HIPCHK(c, hipMemcpyAsync(out8, c->d_rgba, npix * 4, hipMemcpyDeviceToHost, c->stream));
     if (outf) HIPCHK(c, hipMemcpyAsync(outf, c->d_f32, npix * 16, hipMemcpyDeviceToHost, c->stream));
-    if ((r = finish_frame(c)) != RRTE_OK) return r;
+    if ((r = finish_frame(c, true)) != RRTE_OK) return r;
     c->stats.frames++;
     return RRTE_OK;
 }
@@ -1915,6 +1972,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
     if (const char* g = getenv("RRTE_ZC_TILE_SHIFT"))
         c->zc_tile_shift = std::max(3u, std::min(5u, (uint32_t)strtoul(g, nullptr, 0)));
+    if (const char* g = getenv("RRTE_ZC_SYSTEM_STORE")) c->env_zc_system_store = g[0] != '0';
     if (const char* g = getenv("RRTE_NOCOMM_WAIT_MS")) c->env_nocomm_wait_ms = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
         c->env_tile_order = g[0] != '0';
@@ -1950,6 +2008,11 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if ((e = hipMemset(c->d_counters, 0, kCounterBytes)) != hipSuccess) return bail(e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_counters), kCounterBytes, hipHostMallocDefault)) != hipSuccess) return bail(e);
     memset(c->h_counters, 0, kCounterBytes);
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_counters2), kCounterBytes, hipHostMallocDefault)) != hipSuccess) return bail(e);
+    memset(c->h_counters2, 0, kCounterBytes);
+    for (hipEvent_t& ev : c->ev_ctr)
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bail(e);
+    if ((e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) != hipSuccess) return bail(e);
     if (c->fault_stall_at) {
         if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_stall), 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return bail(e);
@@ -1997,6 +2060,10 @@ void rrte_hip_destroy(rrte_ctx* c) {
     for (uint32_t* b : c->d_slab)
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->h_counters2) (void)hipHostFree(c->h_counters2);
+    for (hipEvent_t e : c->ev_ctr)
+        if (e) (void)hipEventDestroy(e);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->h_stall) (void)hipHostFree(c->h_stall);
     for (auto& tp : c->tprof) {
         if (tp.working) tp.work.wait();
@@ -2139,6 +2206,9 @@ rrte_status rrte_hip_set_jit(rrte_ctx* c, int mode) {
 
 rrte_status rrte_hip_stats(rrte_ctx* c, rrte_stats* out) {
     if (!c || !out) return RRTE_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    rrte_status r = resolve_counters(c);
+    if (r != RRTE_OK) return r;
     *out = c->stats;
     return RRTE_OK;
 }
