@@ -575,6 +575,9 @@ rrte_status validate(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_para
     if (p->samples_per_pixel == 0) return fail(c, RRTE_INVALID_ARG, "samples_per_pixel must be >= 1");
     if (p->mode > RRTE_MODE_LAMBERT_SHADOW) return fail(c, RRTE_INVALID_ARG, "unknown mode %u", p->mode);
     if (p->jitter > RRTE_JITTER_RANDOM) return fail(c, RRTE_INVALID_ARG, "unknown jitter %u", p->jitter);
+    // (the high bits are the library's own per-launch flags, kFlagSlabRgb24 / kFlagHostStore)
+    if (p->flags & ~(uint32_t)(RRTE_FLAG_F32_LINEAR | RRTE_FLAG_GATHER_OVERLAP))
+        return fail(c, RRTE_INVALID_ARG, "unknown flags 0x%x", p->flags);
     if ((s->num_prims && !s->prims) || (s->num_lights && !s->lights) || (s->num_materials && !s->materials) ||
         (s->num_sdf_nodes && !s->sdf_nodes))
         return fail(c, RRTE_INVALID_ARG, "null array with nonzero count");
