@@ -1974,7 +1974,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if (const char* g = getenv("RRTE_BATCH_LAUNCH")) c->env_batch_launch = g[0] != '0';
     if (const char* g = getenv("RRTE_BND_ZEROCOPY")) c->env_bnd_zerocopy = g[0] != '0';
     if (const char* g = getenv("RRTE_ZC_TILE_SHIFT"))
-        c->zc_tile_shift = std::max(3u, std::min(5u, (uint32_t)strtoul(g, nullptr, 0)));
+        c->zc_tile_shift = std::max(3u, std::min(6u, (uint32_t)strtoul(g, nullptr, 0)));
     if (const char* g = getenv("RRTE_ZC_SYSTEM_STORE")) c->env_zc_system_store = g[0] != '0';
     if (const char* g = getenv("RRTE_NOCOMM_WAIT_MS")) c->env_nocomm_wait_ms = (uint32_t)strtoul(g, nullptr, 0);
     if (const char* g = getenv("RRTE_TILE_ORDER")) {
