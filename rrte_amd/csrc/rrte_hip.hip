@@ -235,7 +235,7 @@ struct rrte_ctx {
     bool env_bnd_zerocopy = true;
     uint32_t tile_shift = 3;          // tile shape of the launch being planned (KParams::tile_shift)
     bool env_zc_system_store = true;  // ... their pixel stores at system scope (RRTE_ZC_SYSTEM_STORE=0: plain, A/B)
-    uint32_t zc_tile_shift = 5;       // ... of zero-copy blocking frames (RRTE_ZC_TILE_SHIFT: 3 / 4 / 5)
+    uint32_t zc_tile_shift = 5;       // ... of zero-copy blocking frames (RRTE_ZC_TILE_SHIFT: 3 / 4 / 5 / 6)
     struct HostReg { void* p; size_t bytes; };
     std::vector<HostReg> host_regs;   // rrte_hip_host_register'ed ranges (unregistered at destroy)
     struct { uint64_t gen; int mode, jit_mode; bool cull, single, topo, uniform, valid; JitKernel* k; } jit_last{};

@@ -25,6 +25,7 @@ frames = {}
 for label, reg in (("reused", False), ("registered", True)):
     if reg:
         ctx.check(lib.rrte_hip_host_register(ctx.h, buf.ctypes.data, buf.nbytes))
+        buf[:] = 0  # (so the comparison below shows the zero-copy frames' own bytes)
     for _ in range(5):
         ctx.check(lib.rrte_hip_render(ctx.h, sc.ref(), C.byref(prm), ptr))
     t = time.perf_counter()
