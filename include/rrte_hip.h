@@ -281,7 +281,10 @@ const char* rrte_hip_last_error(const rrte_ctx* ctx);
 
 /* Raytracer::render: blocking; writes W*H*4 bytes to host `out_rgba8`.  When `out_rgba8` is pinned
  * host memory (hipHostMalloc'd, or a range registered with rrte_hip_host_register) the kernel stores
- * the frame straight into it while it renders; pageable memory gets one D2H copy after the render. */
+ * the frame straight into it while it renders (system-scope, write-through stores); pageable memory
+ * gets one D2H copy after the render.  Returns when the frame is complete; the frame's statistics
+ * (shadow-ray count) are read back behind it and rrte_hip_stats waits for them.  params->flags takes
+ * only the RRTE_FLAG_* bits (others: RRTE_INVALID_ARG). */
 rrte_status rrte_hip_render(rrte_ctx* ctx, const rrte_scene_ir* scene,
                             const rrte_render_params* params, uint8_t* out_rgba8);
 
@@ -308,6 +311,7 @@ rrte_status rrte_hip_synchronize(rrte_ctx* ctx);
  * while any of it is still running, else 0.  Does not flush an open gather batch. */
 rrte_status rrte_hip_query(rrte_ctx* ctx, uint32_t* busy);
 
+/* The last frame's statistics (after a blocking frame: waits for its counter read-back). */
 rrte_status rrte_hip_stats(rrte_ctx* ctx, rrte_stats* out);
 
 /* Scene-specialised kernels (hiprtc).  OFF: always the
