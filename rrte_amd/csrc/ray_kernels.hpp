@@ -123,6 +123,24 @@ struct SceneValues {
     const rrte_sdf_node* nodes;
 };
 
+// A record of the uploaded scene read through the constant address space: a topology kernel's records
+// are wave-uniform and read-only, but the compiler cannot prove that for plain global loads in a kernel
+// that also stores (it issued them as vector loads: 0.10 -> 0.72 M VMEM reads per 1080p launch against
+// the full kernel); loads from address space 4 at a uniform address are scalar loads.  Word-wise, so
+// that only the words used are loaded.
+template <class T>
+__device__ __forceinline__ T load_uniform(const T* p) {
+    static_assert(sizeof(T) % 4u == 0u, "records are whole dwords");
+    typedef const __attribute__((address_space(4))) uint32_t CWord;
+    CWord* w = (CWord*)p;
+    T v;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+    for (uint32_t k = 0; k < sizeof(T) / 4u; ++k) d[k] = w[k];
+    return v;
+}
+struct NodeArgs { float f[12]; };
+
 // Scene record accessors.  For a full static scene the record is copied in a
 // constexpr-expression context (constexpr local): device-side copies of
 // constexpr globals may be emitted as externally-initialised memory whose
@@ -149,7 +167,7 @@ template <class S, uint32_t I>
 __device__ __forceinline__ DPrim prim_at(const S& sc, UC<I>) {
     if constexpr (S::kTopo) {
         constexpr TopoPrim tp = S::topo_prims[I];
-        DPrim v = sc.prims[I];
+        DPrim v = load_uniform(sc.prims + I);
         v.kind = tp.kind;
         v.sdf_first = tp.sdf_first;
         v.sdf_count = tp.sdf_count;
@@ -169,7 +187,7 @@ constexpr uint32_t light_kind() {
 template <class S, uint32_t I>
 __device__ __forceinline__ DLight light_at(const S& sc, UC<I>) {
     if constexpr (S::kTopo) {
-        DLight v = sc.lights[I];
+        DLight v = load_uniform(sc.lights + I);
         v.kind = light_kind<S, I>();
         return v;
     } else {
@@ -563,7 +581,8 @@ __device__ __forceinline__ void sdf_static_range(const S& sc, G& gp, float* vs, 
             float r;
             bool taken;
             if constexpr (S::kTopo) {
-                taken = sdf_guard(gp, gop, sc.nodes[FIRST + link - 1u].f, vs[sp - 1], p, r);
+                const NodeArgs na = load_uniform(reinterpret_cast<const NodeArgs*>(sc.nodes[FIRST + link - 1u].f));
+                taken = sdf_guard(gp, gop, na.f, vs[sp - 1], p, r);
             } else {
                 constexpr rrte_sdf_node g = S::nodes[FIRST + link - 1u];
                 taken = sdf_guard(gp, gop, g.f, vs[sp - 1], p, r);
@@ -573,7 +592,8 @@ __device__ __forceinline__ void sdf_static_range(const S& sc, G& gp, float* vs, 
             sdf_static_range<S, FIRST, link, END, true>(sc, gp, vs, ps, sp, pp, p);
         } else {
             if constexpr (S::kTopo) {
-                sdf_node_step(gp, tn.op, tn.i, sc.nodes[FIRST + I].f, vs, ps, sp, pp, p);
+                const NodeArgs na = load_uniform(reinterpret_cast<const NodeArgs*>(sc.nodes[FIRST + I].f));
+                sdf_node_step(gp, tn.op, tn.i, na.f, vs, ps, sp, pp, p);
             } else {
                 constexpr rrte_sdf_node n = S::nodes[FIRST + I];
                 sdf_node_step(gp, n.op, n.i, n.f, vs, ps, sp, pp, p);
@@ -591,7 +611,7 @@ struct SdfStaticProgram {
     // program's first node's spare slot f[11] for a topology scene (rrte_hip.hip upload_scene)
     __device__ __forceinline__ float leaf_scale() const {
         if constexpr (S::kTopo) {
-            return sc.nodes[FIRST].f[11];
+            return load_uniform(reinterpret_cast<const NodeArgs*>(sc.nodes[FIRST].f)).f[11];
         } else {
             constexpr float k = sdf_leaf_scale(S::nodes + FIRST, COUNT);
             return k;
