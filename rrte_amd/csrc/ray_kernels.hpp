@@ -439,14 +439,17 @@ struct SdfProgramT {
         // per-node loop, no dynamically indexed stack, and the nodes' scalar loads do not depend on
         // a loop counter (the march loop around this call can keep them in SGPRs).  Same operations
         // in the same order as the loop below, so the same bits.
-        const uint32_t op0 = nodes[0].op;
-        if (RRTE_SDF_FASTPATH && count == 1u && op0 < 32u) return sdf_leaf(g, op0, nodes[0].f, p);
-        if (RRTE_SDF_FASTPATH && count == 3u && op0 < 32u && nodes[1].op < 32u && nodes[2].op >= 32u && nodes[2].op < 64u &&
-            nodes[1].i[2] == 0u) {
-            const float a = sdf_leaf(g, op0, nodes[0].f, p);
-            const float b = sdf_leaf(g, nodes[1].op, nodes[1].f, p);
-            const float k = nodes[2].f[0];
-            switch (nodes[2].op) {
+        // (the program's nodes are wave-uniform: read through load_uniform, scalar loads)
+        const rrte_sdf_node n0 = load_uniform(nodes);
+        const uint32_t op0 = n0.op;
+        if (RRTE_SDF_FASTPATH && count == 1u && op0 < 32u) return sdf_leaf(g, op0, n0.f, p);
+        const rrte_sdf_node n1 = load_uniform(nodes + (count > 1u ? 1u : 0u));
+        const rrte_sdf_node n2 = load_uniform(nodes + (count > 2u ? 2u : 0u));
+        if (RRTE_SDF_FASTPATH && count == 3u && op0 < 32u && n1.op < 32u && n2.op >= 32u && n2.op < 64u && n1.i[2] == 0u) {
+            const float a = sdf_leaf(g, op0, n0.f, p);
+            const float b = sdf_leaf(g, n1.op, n1.f, p);
+            const float k = n2.f[0];
+            switch (n2.op) {
             case RRTE_SDF_UNION: return smn(a, b);
             case RRTE_SDF_DIFFERENCE: return smx(a, -b);
             case RRTE_SDF_INTERSECTION: return smx(a, b);
@@ -459,14 +462,18 @@ struct SdfProgramT {
         f3 ps[(F & kFeatDeform) ? RRTE_SDF_MAX_POINT_STACK : 1];
         uint32_t sp = 0, pp = 0;
         for (uint32_t i = 0; i < count; ++i) {
-            const uint32_t link = nodes[i].i[2];
+            const rrte_sdf_node ni = load_uniform(nodes + i);
+            const uint32_t link = ni.i[2];
             float r;
-            if (link != 0u && sdf_guard(g, nodes[link - 1u].op, nodes[link - 1u].f, vs[sp - 1], p, r)) {
-                vs[sp - 1] = r;
-                i = link - 1u;  // continue after the op
-                continue;
+            if (link != 0u) {
+                const rrte_sdf_node gn = load_uniform(nodes + (link - 1u));
+                if (sdf_guard(g, gn.op, gn.f, vs[sp - 1], p, r)) {
+                    vs[sp - 1] = r;
+                    i = link - 1u;  // continue after the op
+                    continue;
+                }
             }
-            sdf_node_step<G, (F & kFeatDeform) != 0u>(g, nodes[i].op, nodes[i].i, nodes[i].f, vs, ps, sp, pp, p);
+            sdf_node_step<G, (F & kFeatDeform) != 0u>(g, ni.op, ni.i, ni.f, vs, ps, sp, pp, p);
         }
         return vs[0];
     }
@@ -487,15 +494,15 @@ using SdfProgram = SdfProgramT<kFeatAll>;
 template <uint32_t OP>
 struct SdfLeafProgram {
     static constexpr bool kSmall = true;
-    const rrte_sdf_node* __restrict__ node;
+    NodeArgs a;  // the node's arguments (load_uniform)
     __device__ __forceinline__ float leaf_scale() const {
         float k = 0.0f;
 #pragma unroll
-        for (int j = 0; j < 7; ++j) k += node->f[j] < 0.0f ? -node->f[j] : node->f[j];
+        for (int j = 0; j < 7; ++j) k += a.f[j] < 0.0f ? -a.f[j] : a.f[j];
         return k;
     }
     template <class G>
-    __device__ __forceinline__ float eval(f3 p, G& g) const { return sdf_leaf(g, OP, node->f, p); }
+    __device__ __forceinline__ float eval(f3 p, G& g) const { return sdf_leaf(g, OP, a.f, p); }
     __device__ __forceinline__ float operator()(f3 p) const {
         GuardNow g;
         return eval(p, g);
@@ -1326,7 +1333,7 @@ __device__ __forceinline__ bool isect_mesh(const DPrim& pr, const MeshView& mv, 
 template <bool NEED_HIT, class S, bool ANY = false>
 __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t_max,
                                              Hit& out) {
-    const DPrim& pr = sc.prims[i];
+    const DPrim pr = load_uniform(sc.prims + i);  // (i is wave-uniform: scalar loads)
     constexpr uint32_t F = S::kFeat;
     // (a kind outside the variant's features cannot occur: the host picked the variant from the scene)
     if (pr.kind == RRTE_PRIM_SPHERE) return isect_sphere<NEED_HIT, ANY>(pr, r, t_min, t_max, out);
@@ -1335,12 +1342,14 @@ __device__ __forceinline__ bool intersect_at(const S& sc, uint32_t i, const Ray&
             const rrte_sdf_node* nd = sc.nodes + pr.sdf_first;
             if (RRTE_SDF_LEAF_DISPATCH && pr.sdf_count == 1u) {
                 bool hit = false;
+                const rrte_sdf_node n = load_uniform(nd);
                 auto leaf = [&](auto opc) {
                     constexpr uint32_t OP = decltype(opc)::value;
-                    if (nd->op == OP)
+                    if (n.op == OP)
                         hit = isect_sdf<NEED_HIT, SdfLeafProgram<OP>, ANY,
                                         (ANY ? kSecantExit >= 1 : kSecantExit >= 2) && leaf_convex<OP>()>(
-                            pr, SdfLeafProgram<OP>{nd}, r, t_min, t_max, out);
+                            pr, SdfLeafProgram<OP>{load_uniform(reinterpret_cast<const NodeArgs*>(nd->f))}, r, t_min,
+                            t_max, out);
                 };
                 static_for_leaves(leaf);
                 return hit;
@@ -1430,7 +1439,7 @@ __device__ __forceinline__ int closest_t(const S& sc, const Ray& r, float t_min,
 template <class S>
 __device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray& r, float t_min, float t,
                                               uint32_t sub, Hit& out) {
-    const DPrim& pr = sc.prims[i];
+    const DPrim pr = load_uniform(sc.prims + i);  // (i is wave-uniform: scalar loads)
     constexpr uint32_t F = S::kFeat;
     if (pr.kind == RRTE_PRIM_SPHERE) {
         sphere_attributes(pr, r, t, out);
@@ -1440,9 +1449,12 @@ __device__ __forceinline__ void attributes_at(const S& sc, uint32_t i, const Ray
         if (pr.kind == RRTE_PRIM_SDF) {
             const rrte_sdf_node* nd = sc.nodes + pr.sdf_first;
             if (RRTE_SDF_LEAF_DISPATCH && pr.sdf_count == 1u) {
+                const rrte_sdf_node n = load_uniform(nd);
                 auto leaf = [&](auto opc) {
                     constexpr uint32_t OP = decltype(opc)::value;
-                    if (nd->op == OP) sdf_hit_attributes(SdfLeafProgram<OP>{nd}, r, t, out);
+                    if (n.op == OP)
+                        sdf_hit_attributes(SdfLeafProgram<OP>{load_uniform(reinterpret_cast<const NodeArgs*>(nd->f))}, r,
+                                           t, out);
                 };
                 static_for_leaves(leaf);
                 return;
@@ -2060,8 +2072,9 @@ __device__ __forceinline__ Col shade_lambert(const S& sc, const KParams& kp, con
             const float4 bnd = cull_on(cl) ? load_bound(cl) : float4{};
 #pragma unroll 1
             for (uint32_t li = 0; li < sc.num_lights; ++li) {
-                const uint64_t sm = shadow_cull(cl, hb, sc.lights[li], bnd);
-                if (kShadeAll || hit) shade(sc.lights[li], sm, li);
+                const DLight lt = load_uniform(sc.lights + li);  // (li uniform: scalar loads)
+                const uint64_t sm = shadow_cull(cl, hb, lt, bnd);
+                if (kShadeAll || hit) shade(lt, sm, li);
             }
         }
     }
@@ -2323,14 +2336,24 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
 
 // Generic kernel: the scene is read from HBM through wave-uniform (scalar) loads; F = the features
 // compiled in (kFeat*, a superset of the scene's).
-// Register budget of the generic kernel: at least 5 waves per SIMD (<= 96 VGPRs, a few spills) instead
-// of the compiler's 4 (119 VGPRs): frames in a stream -0.05 ms (0.172 -> 0.164 ms per 1080p showcase
-// frame), a lone launch +13 % (6 waves spill too much: 0.216 ms)
+// Register budget of the generic kernel (waves per SIMD it must fit): 5 (<= 96 VGPRs, a few spills)
+// instead of the compiler's 4 -- frames in a stream 0.172 -> 0.164 ms per 1080p showcase frame, a lone
+// launch +13 % -- and, once the scene records were scalar loads, 6 (<= 80 VGPRs) for LAMBERT_SHADOW
+// variants without meshes or deformers: 0.139 -> 0.131 ms; with meshes (+39 %), deformers (+5 %) or the
+// REFCOMPAT stock config (+1 %) 6 waves lose, so those keep 5 (tools/mw_check.sh)
 #ifndef RRTE_GENERIC_MINWAVES
 #define RRTE_GENERIC_MINWAVES 5
 #endif
+#ifndef RRTE_GENERIC_MINWAVES_PLAIN
+#define RRTE_GENERIC_MINWAVES_PLAIN 6
+#endif
+template <int MODE, uint32_t F>
+constexpr int generic_min_waves() {
+    return MODE == RRTE_MODE_LAMBERT_SHADOW && (F & (kFeatMesh | kFeatDeform)) == 0u ? RRTE_GENERIC_MINWAVES_PLAIN
+                                                                                        : RRTE_GENERIC_MINWAVES;
+}
 template <int MODE, bool CULL, uint32_t F = kFeatAll>
-__global__ __launch_bounds__(kBlockThreads, RRTE_GENERIC_MINWAVES) void ray_kernel(KParams kp, SceneView sc, Cull cl, uint32_t* __restrict__ out_rgba8,
+__global__ __launch_bounds__(kBlockThreads, (generic_min_waves<MODE, F>())) void ray_kernel(KParams kp, SceneView sc, Cull cl, uint32_t* __restrict__ out_rgba8,
                                                   float4* __restrict__ out_f32,
                                                   unsigned long long* __restrict__ counters) {
     SceneViewF<F> s;

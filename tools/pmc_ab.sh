@@ -7,6 +7,7 @@
 # time; the disk-cache key includes the options).  Output: gpurun_out/pmc_ab/<name>_r<k>/ and a table
 # on stdout.  Every step has its own time limit; the first failure ends the run.  PMC_COUNTERS replaces
 # the counter set (one pass; e.g. "FETCH_SIZE" or "WRITE_SIZE" -- the block limits of rocprofv3 apply).
+# A variant's BENCH_ARGS=... (no spaces: e.g. BENCH_ARGS=--jit=off) passes to bench.py.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 ROUNDS=${1:?rounds}; shift
@@ -18,13 +19,14 @@ COUNTERS=${PMC_COUNTERS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_
 for k in $(seq 1 $ROUNDS); do
   for spec in "$@"; do
     name=${spec%%|*}; envs=${spec#*|}
+    bargs=$(echo "$envs" | tr ' ' '\n' | sed -n 's/^BENCH_ARGS=//p')
     d=$OUT/${name}_r$k; mkdir -p $d
     for steps in 200 20; do
-      env $envs timeout -k 10 180 python3 $R/bench.py --no-cpu --no-stock --no-boundary --steps $steps > $d/bench$steps.log 2>&1 \
+      env $envs timeout -k 10 180 python3 $R/bench.py --no-cpu --no-stock --no-boundary $bargs --steps $steps > $d/bench$steps.log 2>&1 \
         || { tail $d/bench$steps.log; echo "bench failed: $name"; exit 1; }
     done
     # (the program itself right after --: env assignments are exported before rocprofv3 starts)
-    ( [ -n "$envs" ] && export $envs; timeout -s KILL 120 rocprofv3 --pmc $COUNTERS --output-format csv -d $d/pmc -o run -- python3 $R/bench.py --no-cpu --no-stock --no-boundary --steps 20 > $d/pmc.log 2>&1 ) \
+    ( [ -n "$envs" ] && export $envs; timeout -s KILL 120 rocprofv3 --pmc $COUNTERS --output-format csv -d $d/pmc -o run -- python3 $R/bench.py --no-cpu --no-stock --no-boundary $bargs --steps 20 > $d/pmc.log 2>&1 ) \
       || { tail $d/pmc.log; echo "pmc failed: $name"; exit 1; }
     python3 - "$d" "$name" "$k" <<'PY'
 import csv, json, sys, collections
