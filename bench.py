@@ -602,7 +602,8 @@ def main():
         kinds = kernel_variants(scene, prm, fulls, sptrs, dev, W * H * prm.samples_per_pixel + shadow // args.steps,
                                 anim=anim)
 
-    # the reference's stock config on the generic kernel (rank 0, N=1 only; not the headline)
+    # the reference's stock config (rank 0, N=1 only; not the headline) on the headline's context: its
+    # own scene-specialised REFCOMPAT kernel (runtime sample / bounce loops), compiled on the warm-up frames
     stock = None
     if world == 1 and not args.no_stock:
         sscene, sprm = stock_config(args)

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Generic kernel (bench.py --jit off) at two register budgets on scenes beyond the headline (960x540),
-# and the stock config's secondary number (the generic kernel, REFCOMPAT spp 4 depth 50).
+# and the stock config's secondary number (REFCOMPAT spp 4 depth 50 -- on the scene-specialised kernel,
+# so a control: the library build changes only the generic kernel).
 # usage: tools/mw_check.sh LIB_A LIB_B   (paths of librrte_hip builds; "" = the default library)
 set -o pipefail
 for lib in "$@"; do
