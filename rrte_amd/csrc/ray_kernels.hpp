@@ -2340,7 +2340,8 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
 // instead of the compiler's 4 -- frames in a stream 0.172 -> 0.164 ms per 1080p showcase frame, a lone
 // launch +13 % -- and, once the scene records were scalar loads, 6 (<= 80 VGPRs) for LAMBERT_SHADOW
 // variants without meshes or deformers: 0.139 -> 0.131 ms; with meshes (+39 %) or deformers (+5 %) 6 waves
-// lose, so those keep 5, as do the REFCOMPAT variants (not measured at 6; DESIGN.md §13, tools/mw_check.sh)
+// lose, so those keep 5, as do the REFCOMPAT variants (6 waves: one sample -3 %, the reference's stock config
+// spp 4 / depth 50 +6 %; DESIGN.md §13, tools/mw_check.sh, tools/refc_check.sh)
 #ifndef RRTE_GENERIC_MINWAVES
 #define RRTE_GENERIC_MINWAVES 5
 #endif
