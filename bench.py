@@ -585,6 +585,16 @@ def main():
         reg_ms = (time.perf_counter() - a) / nb * 1e3
         reg_ok = bool(np.array_equal(reg, hbuf))
         ctx.check(lib.rrte_hip_host_unregister(ctx.h, reg.ctypes.data))
+        # a buffer the engine allocates page-locked (hipHostMalloc; torch's pinned memory is): zero copy too
+        pin = torch.zeros(W * H * 4, dtype=torch.uint8, pin_memory=True)
+        ppin = C.cast(C.c_void_p(pin.data_ptr()), C.POINTER(C.c_uint8))
+        for _ in range(3):
+            ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), ppin))
+        a = time.perf_counter()
+        for _ in range(nb):
+            ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), ppin))
+        pin_ms = (time.perf_counter() - a) / nb * 1e3
+        pin_ok = bool(np.array_equal(pin.numpy(), hbuf))
         boundary = {"entry": "rrte_hip_render (blocking; Raytracer::render's signature, host RGBA8 out, D2H included)",
                     "ms_per_frame_reused_buffer": round(reused_ms, 4),
                     "ms_per_frame_fresh_buffer": round(fresh_ms, 4),
@@ -592,9 +602,12 @@ def main():
                     "ms_per_frame_fresh_pretouched": round(touched_s / nb * 1e3, 4),
                     "ms_per_frame_registered_buffer": round(reg_ms, 4),
                     "registered_equals_copy_path": reg_ok,
+                    "ms_per_frame_hostmalloc_buffer": round(pin_ms, 4),
+                    "hostmalloc_equals_copy_path": pin_ok,
                     "frames": nb, "note": "fresh = a new zeroed W*H*4 buffer per frame, as raytracer.rs:54 allocates; "
                                           "registered = the reused buffer pinned once (rrte_hip_host_register): the "
-                                          "kernel stores the frame into it directly, no D2H copy"}
+                                          "kernel stores the frame into it directly, no D2H copy; hostmalloc = a "
+                                          "frame buffer allocated page-locked (hipHostMalloc), zero copy as well"}
 
     kinds = None
     if world == 1 and not args.no_stock:
