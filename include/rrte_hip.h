@@ -305,6 +305,10 @@ rrte_status rrte_hip_render_f32(rrte_ctx* ctx, const rrte_scene_ir* scene,
 rrte_status rrte_hip_render_async(rrte_ctx* ctx, const rrte_scene_ir* scene,
                                   const rrte_render_params* params, void* d_out_rgba8,
                                   void* d_out_rgba32f, void* stream);
+/* Waits for every frame of the context.  With a communicator the wait is bounded by the comm timeout
+ * (below); without one by env RRTE_NOCOMM_WAIT_MS (default 600000 = 10 minutes, far above any queue
+ * of frames; 0 = no limit): a kernel that never completes returns RRTE_HIP_ERROR instead of hanging.
+ * The same bound applies to rrte_hip_host_unregister's drain. */
 rrte_status rrte_hip_synchronize(rrte_ctx* ctx);
 /* Non-blocking completion test of the work queued on the context's OWN streams (its default stream
  * and the batched-gather render / comm streams; caller streams are the caller's to query): *busy = 1
@@ -372,6 +376,12 @@ rrte_status rrte_hip_build_id(char* out, size_t out_len);
  * (or `headers_override` in their place, to show that a rebuilt library's headers change the key),
  * the hiprtc options (RRTE_JIT_EXTRA_OPTS included) and the hiprtc version. */
 rrte_status rrte_hip_jit_cache_key(const char* source, const char* headers_override, char* out, size_t out_len);
+/* Diagnostic: with env RRTE_DEBUG bit 2 (value 4) set when the context was created, every wave
+ * range-checks the indices it derives from its launch (tile-list slot, decoded tile, frame, output
+ * row) before using them and ORs a code into a device check word instead of an out-of-range access
+ * (1 list slot, 2 tile, 4 frame, 8 output row).  Drains the context's work, returns the word in *word
+ * and clears it.  0 = no violation. */
+rrte_status rrte_hip_check_word(rrte_ctx* ctx, uint64_t* word);
 
 /* ----------------------------------------------------- multi-GPU (RCCL/xGMI) */
 /* Row-band partition: band b (band_rows rows) belongs to rank b % nranks.

@@ -2172,6 +2172,31 @@ __device__ __forceinline__ LaunchTile launch_tile(const KParams& kp) {
     return t;
 }
 
+// RRTE_DEBUG bit 2: the launch's derived indices, checked before any memory access that uses them.
+// Check-word bits: 1 list slot out of range, 2 decoded tile outside the launch's tiles, 4 frame index
+// >= nframes, 8 an output row outside the frame.
+__device__ __noinline__ bool launch_indices_ok(const KParams& kp, unsigned long long* counters) {
+    uint32_t bad = 0u;
+    const uint32_t th = 64u >> kp.tile_shift, gy = (kp.rows + th - 1u) / th;
+    const uint32_t k = blockIdx.z * kp.tiles_x + blockIdx.x;
+    if (blockIdx.y >= kp.nframes || blockIdx.y >= kMaxLaunchFrames) bad |= 4u;
+    if (kp.hot) {
+        if (k < kp.hot_n) {
+            const uint32_t at = (k & 7u) * kp.hot_stride + (k >> 3);
+            if (kp.hot_stride * 8u < kp.hot_n || at >= kp.hot_stride * 8u) bad |= 1u;
+            else {
+                const uint32_t h = kp.hot[at];
+                if (hot_x(h) >= kp.tiles_x || hot_y(h) >= gy) bad |= 2u;
+            }
+        }
+    } else if (blockIdx.x >= kp.tiles_x || blockIdx.z >= gy) {
+        bad |= 2u;
+    }
+    if (!bad && kp.rows && kp.band_rows == 0u && kp.row0 + kp.rows > kp.height) bad |= 8u;
+    if (bad && (threadIdx.x & 63u) == 0u) atomicOr(counters + 1, (unsigned long long)bad);
+    return bad == 0u;
+}
+
 // One lane per pixel; wave = workgroup = 8x8 tile (RRTE_WG256: 16x16-pixel workgroups).  Every lane
 // of a wave runs the sample loop (lanes past the image edge are idle but
 // present) so the culling reductions see converged waves.  CULL selects the
@@ -2181,6 +2206,10 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
                                                 uint32_t* __restrict__ out_rgba8, float4* __restrict__ out_f32,
                                                 unsigned long long* __restrict__ counters) {
     const uint32_t lane = threadIdx.x & 63u, wave = kWg64 ? 0u : threadIdx.x >> 6;
+    // RRTE_DEBUG bit 2 (diagnostics): every index this wave derives from the launch (list slot, tile,
+    // frame) is range-checked before use; a violation sets a bit in the check word (counters[1], an
+    // unused word of shard 0; rrte_hip_check_word) and the wave stops instead of touching memory
+    if ((kp.debug & 4u) && kWg64 && !launch_indices_ok(kp, counters)) return;
     const LaunchTile tile = launch_tile(kp);
     if (!tile.run) return;
     // frame tile.z of the launch: its camera, its output (multi-frame launches have no f32 output)
@@ -2201,9 +2230,13 @@ __device__ __forceinline__ void ray_kernel_body(const KParams& kp, const S& sc, 
     const uint32_t ts = kp.tile_shift;  // (kWg64: tile 1 << ts wide, 64 >> ts rows)
     const uint32_t x = kWg64 ? (tile.x << ts) + (lane & ((1u << ts) - 1u)) : tile.x * 16u + (wave & 1u) * 8u + (lane & 7u);
     const uint32_t lr = kWg64 ? brow * (64u >> ts) + (lane >> ts) : brow * 16u + (wave >> 1) * 8u + (lane >> 3);
-    const bool live = x < kp.width && lr < kp.rows;
+    bool live = x < kp.width && lr < kp.rows;
     const uint32_t xc = live ? x : 0u;
     const uint32_t y = image_row(kp, live ? lr : 0u);
+    if ((kp.debug & 4u) && live && y >= kp.height) {  // (bit 2: a band mapping past the frame)
+        atomicOr(counters + 1, 8ull);
+        live = false;
+    }
     const uint32_t pix = y * kp.width + xc;
     uint32_t nshadow = 0;
     Col acc{0.0f, 0.0f, 0.0f, 1.0f};  // BLACK

@@ -124,6 +124,10 @@ struct rrte_ctx {
     hipEvent_t ev_done = nullptr;     // the blocking frame complete (before its counter copy)
     bool ctr_pending = false;         // the last frame's counts are in slot ctr_slot, not yet in stats
     int ctr_slot = 0;
+    // streams that have waited for the pending counter copy (issue_launch): a frame launched on another
+    // stream than the context's must not add shadow rays to the counters while the blocking frame's
+    // snapshot of them is still being copied
+    std::vector<hipStream_t> ctr_ordered;
     // multi-GPU
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -331,10 +335,14 @@ struct rrte_ctx {
     hipEvent_t ev_bcopy = nullptr;
     bool env_tile_order = true;
     bool env_tile_order_fixed = false;  // RRTE_TILE_ORDER=2: a fixed scrambled permutation of the tiles (tests)
-    uint32_t env_nocomm_wait_ms = 0;    // RRTE_NOCOMM_WAIT_MS: limit of device waits without a communicator (0 = none)
+    // RRTE_NOCOMM_WAIT_MS: limit of device waits without a communicator (0 = none).  Nothing can stall
+    // a frame without one, so the default is far above any frame (10 minutes): a hung or faulted kernel
+    // still ends rrte_hip_synchronize / host_unregister / destroy with RRTE_HIP_ERROR
+    uint32_t env_nocomm_wait_ms = 600000;
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
     // per launch, so the version pool wraps within a few frames)
     bool env_test_recycle = false;
+    bool env_fault_bad_slot = false;  // RRTE_FAULT_BAD_SLOT=1 (tests, only with RRTE_DEBUG bit 2): slot 0 of every uploaded list names a tile outside the frame
     // band partition of the last multi-GPU frame (frame_band_map)
     struct {
         bool valid = false;
@@ -1543,6 +1551,8 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
     if (tp.cap_h_list[pick] < words) return false;  // (reserve_hot_lists could not grow it yet)
     uint32_t* stage = tp.h_list[pick];
     for (size_t k = 0; k < n; ++k) stage[(k & 7u) * stride + (k >> 3)] = tp.slots[k];
+    // fault injection for the device index check (tests): only where the check stops the wave first
+    if (c->env_fault_bad_slot && (c->env_debug & 4u) && n) stage[0] = hot_pack(0u, 0xfff0u);
     if (!tp.ev_up[pick] && hipEventCreateWithFlags(&tp.ev_up[pick], hipEventDisableTiming) != hipSuccess) return false;
     if (hipMemcpyAsync(tp.d_list[pick], stage, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
         hipEventRecord(tp.ev_up[pick], tp.upload_stream) != hipSuccess)
@@ -1692,6 +1702,11 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         B.ret.use(st);
     }
     c->launched.use(st);
+    if (c->ctr_pending && st != c->stream &&
+        std::find(c->ctr_ordered.begin(), c->ctr_ordered.end(), st) == c->ctr_ordered.end()) {
+        HIPCHK(c, ev_wait(c, st, c->ev_ctr[c->ctr_slot], "wait counter snapshot"));
+        c->ctr_ordered.push_back(st);
+    }
     const dim3 grid(L.gx, L.k.nframes, L.gy), block(kBlockThreads);
     trace_rec(c, profile ? "launch ray (profiled)" : "launch ray", st, nullptr, L.k.nframes, L.k.rows);
     if (jk) {
@@ -1788,6 +1803,7 @@ rrte_status finish_frame(rrte_ctx* c, bool deferred = false) {
     }
     c->ctr_slot = slot;
     c->ctr_pending = true;
+    c->ctr_ordered.clear();
     if (!deferred && (r = resolve_counters(c)) != RRTE_OK) return r;
     if (c->pending_kernel_timing) {
         float ms = 0.0f;
@@ -1875,7 +1891,7 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
     c->jit_stream = false;  // (one blocking frame: the latency flavour of the specialised kernel)
     // pinned caller buffer: the kernel writes the frame into it directly (no D2H copy afterwards)
     uint32_t* zc = out8 && !outf && c->env_bnd_zerocopy ? pinned_device_ptr(out8, npix * 4) : nullptr;
-    const bool chunked = !zc && out8 && !outf && c->bnd_chunks > 1 && p->height >= 32u && !c->env_debug;
+    const bool chunked = !zc && out8 && !outf && c->bnd_chunks > 1 && p->height >= 32u && !(c->env_debug & ~4u);  // (bit 2, the index check, keeps every path)
     if (chunked) {
         r = render_chunked(c, s, p, out8, (uint32_t)c->bnd_chunks);
     } else {
@@ -1982,6 +1998,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         c->env_tile_order_fixed = g[0] == '2';  // 0 image order, 2 fixed permutation (tests), else measured (default)
     }
     if (const char* g = getenv("RRTE_TEST_RECYCLE")) c->env_test_recycle = g[0] == '1';
+    if (const char* g = getenv("RRTE_FAULT_BAD_SLOT")) c->env_fault_bad_slot = g[0] == '1';
     if (const char* g = getenv("RRTE_BND_CHUNKS"); g && *g)
         c->bnd_chunks = std::max(1, std::min(rrte_ctx::kBndChunksMax, (int)strtol(g, nullptr, 0)));
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
@@ -2173,6 +2190,17 @@ rrte_status rrte_hip_synchronize(rrte_ctx* c) {
         if (b) (void)hipFree(b);
     c->graveyard.clear();
     return finish_frame(c);
+}
+
+rrte_status rrte_hip_check_word(rrte_ctx* c, uint64_t* word) {
+    if (!c || !word) return RRTE_INVALID_ARG;
+    rrte_status r = rrte_hip_synchronize(c);
+    if (r != RRTE_OK) return r;
+    unsigned long long w = 0;  // counters[1]: an unused word of shard 0 (ray_kernels.hpp launch_indices_ok)
+    HIPCHK(c, hipMemcpy(&w, c->d_counters + 1, sizeof w, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemset(c->d_counters + 1, 0, sizeof w));
+    *word = w;
+    return RRTE_OK;
 }
 
 rrte_status rrte_hip_set_comm_timeout(rrte_ctx* c, uint32_t ms) {
@@ -2425,7 +2453,7 @@ rrte_status rrte_hip_comm_init(rrte_ctx* c, int nranks, int rank, const uint8_t 
 // test is on signs only (no host arithmetic to mirror); NaN fails it.  Every rank decides from the
 // same scene and parameters, so all agree on the slab format.  RRTE_GATHER_RGB24=0 forces RGBA8.
 bool slab_rgb24(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p) {
-    if (c->env_gather_rgba || c->env_debug || p->mode != RRTE_MODE_LAMBERT_SHADOW) return false;
+    if (c->env_gather_rgba || (c->env_debug & ~4u) || p->mode != RRTE_MODE_LAMBERT_SHADOW) return false;
     const float thr = p->samples_per_pixel == 1 ? 0.0f : 1.0f;
     if (!(p->background[3] >= thr)) return false;
     for (uint32_t i = 0; i < s->num_materials; ++i)
@@ -2607,8 +2635,9 @@ static rrte_status comm_abort(rrte_ctx* c, const char* why) {
 // instead of blocking, so work that sits behind a gather that never completes -- a dead or stalled
 // peer -- surfaces as RRTE_RCCL_ERROR after comm_timeout_ms (the communicator aborted) instead of a
 // hang.  Without a communicator no gather can stall a frame (an aborted one's kernels are being torn
-// down), so the wait lasts as long as the device needs -- a single-GPU caller may queue minutes of
-// frames -- unless RRTE_NOCOMM_WAIT_MS sets a limit (RRTE_HIP_ERROR after it; 0, the default, = none).
+// down), so the wait lasts as long as the device needs up to RRTE_NOCOMM_WAIT_MS (default 10 minutes,
+// far above any queue of frames; RRTE_HIP_ERROR after it so a hung or faulted kernel still returns;
+// 0 = no limit).
 static rrte_status poll_events(rrte_ctx* c, const hipEvent_t* ev, size_t n) {
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t limit_ms = c->comm ? c->comm_timeout_ms : c->env_nocomm_wait_ms;

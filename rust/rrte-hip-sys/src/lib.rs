@@ -132,6 +132,7 @@ extern "C" {
                                     n_slots: *mut u32) -> rrte_status;
     pub fn rrte_hip_jit_cache_key(source: *const c_char, headers_override: *const c_char, out: *mut c_char,
                                   out_len: usize) -> rrte_status;
+    pub fn rrte_hip_check_word(ctx: *mut rrte_ctx, word: *mut u64) -> rrte_status;
     pub fn rrte_hip_comm_unique_id(out_id: *mut u8) -> rrte_status;
     pub fn rrte_hip_comm_init(ctx: *mut rrte_ctx, nranks: c_int, rank: c_int, id: *const u8) -> rrte_status;
     pub fn rrte_hip_render_gather(ctx: *mut rrte_ctx, scene: *const rrte_scene_ir,

@@ -268,8 +268,9 @@ def test_local_render_keeps_the_in_place_batch_open(monkeypatch):
 
 def test_wait_without_communicator_is_unbounded(monkeypatch):
     """without a communicator nothing can stall a frame, so rrte_hip_synchronize
-    waits as long as the device needs -- far past the communicator timeout -- and returns RRTE_OK;
-    RRTE_NOCOMM_WAIT_MS is an opt-in limit (RRTE_HIP_ERROR once it expires)."""
+    waits as long as the device needs -- far past the communicator timeout -- and returns RRTE_OK.
+    ADVICE r05 (low): the wait keeps a limit far above any frame (RRTE_NOCOMM_WAIT_MS, default 10
+    minutes, 0 = none) so a hung kernel still returns; a short limit returns RRTE_HIP_ERROR."""
     import torch
     objs, lights, cam, cfg = scenes.deformation_stress(1920, 1080)
     sc, prm = LoweredScene(objs, lights, cam), cfg.lower()
