@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--flyby", type=int, default=0,
                     help="camera fly-by: frame i renders camera pose i %% K of K poses orbiting the scene's target "
                          "(0.6 degrees apart; pose 0 = the scene's own camera); 0 = static camera")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the secondary BASELINE configs (basic-demo 640x480, advanced-demo 1080p, "
+                         "sdf-showcase 4K, deformation stress 4K) measured beside the headline at N = 1")
     ap.add_argument("--jit", default="on", choices=["on", "off", "auto"],
                     help="scene-specialised kernel (hiprtc, compiled during warm-up) or the generic kernel")
     return ap.parse_args()
@@ -340,6 +343,107 @@ def stock_config(args):
     objs, lights, cam, cfg = scenes.SCENES[args.scene](args.width, args.height, mode="refcompat")
     cfg.samples_per_pixel, cfg.max_depth, cfg.jitter = 4, 50, "random"
     return LoweredScene(objs, lights, cam), cfg.lower()
+
+
+# The other BASELINE.json configs at N = 1, measured the way the headline is: frames in
+# flight on the scene-specialised kernel, HIP-event launch time for the VALU roofline, the oracle's flop
+# tally, the oracle on the host's threads as the CPU baseline (the same frame doubles as the verification
+# reference), and the PMC summary of the same workload and build when one is committed.
+LEGS = [
+    ("configs[0]", "basic-demo", 640, 480, "refcompat", "basic-demo 640x480 (ground + 3 spheres, the reference's 2 "
+     "point lights), the reference CPU raytracer's formula (REFCOMPAT, max_depth 1)"),
+    ("configs[2]", "advanced-demo", 1920, 1080, "lambert_shadow", "advanced-demo 1920x1080 (6 spheres, 5 point "
+     "lights with shadow rays)"),
+    ("configs[3]", "sdf-showcase", 3840, 2160, "lambert_shadow", "sdf-showcase 3840x2160, the 1-GPU point of the "
+     "2/4/8-GPU row-tiled config"),
+    ("configs[4]", "deformation-stress", 3840, 2160, "lambert_shadow", "deformation stress 3840x2160 (64-node CSG "
+     "under bend -> twist -> 4-octave noise), the 1-GPU point of the 8-GPU config"),
+]
+
+
+def config_leg(name, W, H, mode, dev, cpu_budget_s, flight=4, target_s=0.5):
+    import torch
+    objs, lights, cam, cfg = scenes.SCENES[name](W, H, mode=mode)
+    scene, prm = LoweredScene(objs, lights, cam), cfg.lower()
+    c = Context(dev.index, jit=abi.JIT_ON)
+    lib = c.lib
+    streams = [torch.cuda.Stream(dev) for _ in range(flight)]
+    sp = [C.c_void_p(s.cuda_stream) for s in streams]
+    outs = [torch.empty(W * H, dtype=torch.int32, device=dev) for _ in range(flight)]
+    go = lambda i: c.check(lib.rrte_hip_render_async(c.h, scene.ref(), C.byref(prm), outs[i % flight].data_ptr(),  # noqa: E731
+                                                     None, sp[i % flight]))
+    for i in range(3):  # compile + the first profiled frames
+        go(i)
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    go(0)
+    torch.cuda.synchronize(dev)
+    one = max(time.perf_counter() - t, 1e-6)
+    n = int(min(2000, max(20, target_s / one)))
+    # per launch: frames back to back on one stream between two events
+    n_seq = min(n, 20)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(streams[0])
+    for _ in range(n_seq):
+        go(0)
+    e1.record(streams[0])
+    torch.cuda.synchronize(dev)
+    launch_ms = e0.elapsed_time(e1) / n_seq
+    c.check(lib.rrte_hip_synchronize(c.h))  # fold earlier counts away
+    c.stats()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(n):
+        go(i)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    c.check(lib.rrte_hip_synchronize(c.h))
+    st = c.stats()
+    frames = [o.cpu().numpy().view(np.uint8).copy() for o in outs[:min(flight, n)]]
+    jit_active = int(st.jit_active)
+    c.close()
+    shadow = int(st.shadow_rays)
+    rays = W * H * prm.samples_per_pixel * n + shadow
+    value = rays / elapsed / 1e6
+    # the oracle on the host's threads: whole frames (median of up to 3 within the budget); the last one is
+    # the verification reference
+    import oracle
+    threads = cpu_threads()
+    times, ref = [], None
+    ts0 = time.perf_counter()
+    while len(times) < 3 and (not times or time.perf_counter() - ts0 < cpu_budget_s):
+        a = time.perf_counter()
+        r8, _, rsh = oracle.render(scene, prm, nthreads=threads, want_f32=False)
+        times.append(time.perf_counter() - a)
+        ref = (r8, rsh)
+    cpu_s = statistics.median(times)
+    cpu_value = (W * H * prm.samples_per_pixel + ref[1]) / cpu_s / 1e6
+    flops, _, _ = flop_tally(scene, prm)
+    valu_tf = flops / (launch_ms * 1e-3) / 1e12
+    wl = f"{name}@{W}x{H}/{mode}"
+    pmc, pmc_note = pmc_traffic(wl, abi.build_id())
+    leg = {"workload": None, "value": round(value, 3), "unit": "Mray/s", "ms_per_frame": round(elapsed / n * 1e3, 5),
+           "frames": n, "frames_in_flight": flight, "primary_rays_per_frame": W * H * prm.samples_per_pixel,
+           "shadow_rays_per_frame": shadow / n, "kernel": "rrte_jit_kernel (scene-specialised)" if jit_active else
+           "generic", "avg_launch_ms": round(launch_ms, 5),
+           "roofline": {"bound": "valu", "achieved": round(valu_tf, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": valu_tf / VALU_PEAK_TFLOPS, "flops_per_launch": flops,
+                        "achieved_at_frame_rate": round(flops / (elapsed / n) / 1e12, 3),
+                        "traffic": pmc["hbm_bytes_per_launch"] if pmc else None, "profile": pmc_note,
+                        "hbm": {"achieved": round(4 * W * H / (launch_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": 4 * W * H / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
+           "cpu_baseline": {"value": round(cpu_value, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+                            "sample": f"median of {len(times)} whole {W}x{H} frames, {cpu_s * 1e3:.1f} ms/frame, "
+                                      f"oracle/rrte_oracle.c, {threads} threads"},
+           "verified": verify_frames(frames, shadow, n, ref, refs=None) if n >= len(frames) else None}
+    leg["cpu_baseline"]["gpu_over_cpu"] = round(value / cpu_value, 2)
+    if pmc and pmc.get("valu") is not None:
+        leg["valu"] = {k: pmc["valu"].get(k) for k in ("VALUUtilization_pct", "VALUBusy_pct", "OccupancyPercent",
+                                                        "issue_frac")}
+        cpd = pmc.get("counters_per_dispatch", {})
+        leg["valu"]["SQ_INSTS_VALU"] = cpd.get("SQ_INSTS_VALU")
+        leg["valu"]["SQ_INSTS_SALU"] = cpd.get("SQ_INSTS_SALU")
+    return leg
 
 
 def main():
@@ -635,6 +739,13 @@ def main():
                              "random jitter + scatter (counter-based RNG)",
                  "value": round(W * H * 4 / ts / 1e6, 3), "unit": "Msample/s", "ms_per_frame": round(ts * 1e3, 4)}
 
+    legs = None
+    if world == 1 and not args.no_legs:
+        legs = {}
+        for key, name, lw, lh, lmode, desc in LEGS:
+            legs[key] = config_leg(name, lw, lh, lmode, dev, cpu_budget_s=args.cpu_seconds)
+            legs[key]["workload"] = desc
+
     if rank == 0:
         rays = primary + shadow
         value = rays / elapsed / 1e6
@@ -742,6 +853,8 @@ def main():
             line["boundary"] = boundary
         if kinds is not None:
             line["kernel_kinds"] = kinds
+        if legs is not None:
+            line["configs"] = legs
         if stock is not None:
             line["stock_config"] = stock
         if world == 1 and not args.no_cpu:

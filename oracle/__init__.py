@@ -58,8 +58,8 @@ def load():
     for fn in ("rrte_oracle_sinf", "rrte_oracle_cosf"):
         getattr(lib, fn).restype = C.c_float
         getattr(lib, fn).argtypes = [C.c_float]
-    lib.rrte_oracle_value_noise.restype = C.c_float
-    lib.rrte_oracle_value_noise.argtypes = [C.c_float, C.c_float, C.c_float, C.c_uint32]
+    lib.rrte_oracle_value_noise3.restype = None
+    lib.rrte_oracle_value_noise3.argtypes = [C.c_float, C.c_float, C.c_float, C.c_uint32, C.POINTER(C.c_float)]
     _lib = lib
     return lib
 

@@ -244,30 +244,41 @@ static inline void sincos_rrte(float x, float* s_out, float* c_out) {
 float rrte_oracle_sinf(float x) { float s, c; sincos_rrte(x, &s, &c); return s; }
 float rrte_oracle_cosf(float x) { float s, c; sincos_rrte(x, &s, &c); return c; }
 
-/* Value-noise lattice hash -> [-1, 1). */
-static inline float lattice(int32_t ix, int32_t iy, int32_t iz, uint32_t seed) {
+/* Three-channel value noise (build-defined, DESIGN.md §6 'Deformers'): every lattice corner has ONE
+ * 32-bit hash of (seed, corner) -- the xor of per-axis multiplies, then a 32-bit finaliser -- whose
+ * bits give the corner's three values in [-1, 1): bits 0-10 and 11-21 (11 bits each, step 2^-10) and
+ * bits 22-31 (10 bits, step 2^-9); each channel is interpolated trilinearly with the smoothstep fade
+ * 3t^2 - 2t^3.  (Rounds 1-5 hashed each channel separately; one hash per corner is a third of the
+ * integer work) */
+static inline uint32_t lattice_hash(int32_t ix, int32_t iy, int32_t iz, uint32_t seed) {
     uint32_t h = seed ^ ((uint32_t)ix * 0x8da6b343u) ^ ((uint32_t)iy * 0xd8163841u) ^ ((uint32_t)iz * 0xcb1ab31fu);
     h = (h ^ (h >> 16)) * 0x7feb352du;
     h = (h ^ (h >> 15)) * 0x846ca68bu;
-    h = h ^ (h >> 16);
-    return (float)(h >> 8) * 1.1920928955078125e-7f - 1.0f;
+    return h ^ (h >> 16);
+}
+static inline float lattice_ch(uint32_t h, int k) {
+    if (k == 0) return (float)(h & 0x7ffu) * 0x1p-10f - 1.0f;
+    if (k == 1) return (float)((h >> 11) & 0x7ffu) * 0x1p-10f - 1.0f;
+    return (float)(h >> 22) * 0x1p-9f - 1.0f;
 }
 static inline float lerpf_(float a, float b, float t) { return a + (b - a) * t; }
-float rrte_oracle_value_noise(float x, float y, float z, uint32_t seed) {
+void rrte_oracle_value_noise3(float x, float y, float z, uint32_t seed, float out[3]) {
     float fx0 = floorf(x), fy0 = floorf(y), fz0 = floorf(z);
     int32_t ix = (int32_t)fx0, iy = (int32_t)fy0, iz = (int32_t)fz0;
     float fx = x - fx0, fy = y - fy0, fz = z - fz0;
     float ux = fx * fx * (3.0f - 2.0f * fx);
     float uy = fy * fy * (3.0f - 2.0f * fy);
     float uz = fz * fz * (3.0f - 2.0f * fz);
-    float c000 = lattice(ix, iy, iz, seed), c100 = lattice(ix + 1, iy, iz, seed);
-    float c010 = lattice(ix, iy + 1, iz, seed), c110 = lattice(ix + 1, iy + 1, iz, seed);
-    float c001 = lattice(ix, iy, iz + 1, seed), c101 = lattice(ix + 1, iy, iz + 1, seed);
-    float c011 = lattice(ix, iy + 1, iz + 1, seed), c111 = lattice(ix + 1, iy + 1, iz + 1, seed);
-    float x00 = lerpf_(c000, c100, ux), x10 = lerpf_(c010, c110, ux);
-    float x01 = lerpf_(c001, c101, ux), x11 = lerpf_(c011, c111, ux);
-    float y0 = lerpf_(x00, x10, uy), y1 = lerpf_(x01, x11, uy);
-    return lerpf_(y0, y1, uz);
+    uint32_t h[8];
+    for (int j = 0; j < 8; ++j) h[j] = lattice_hash(ix + (j & 1), iy + ((j >> 1) & 1), iz + ((j >> 2) & 1), seed);
+    for (int k = 0; k < 3; ++k) {
+        float x00 = lerpf_(lattice_ch(h[0], k), lattice_ch(h[1], k), ux);
+        float x10 = lerpf_(lattice_ch(h[2], k), lattice_ch(h[3], k), ux);
+        float x01 = lerpf_(lattice_ch(h[4], k), lattice_ch(h[5], k), ux);
+        float x11 = lerpf_(lattice_ch(h[6], k), lattice_ch(h[7], k), ux);
+        float y0 = lerpf_(x00, x10, uy), y1 = lerpf_(x01, x11, uy);
+        out[k] = lerpf_(y0, y1, uz);
+    }
 }
 
 /* ------------------------------------------------------- SDF evaluator */
@@ -379,16 +390,14 @@ static v3 sdf_deform(const rrte_sdf_node* n, v3 p) {
         uint32_t oct = n->i[0], seed = n->i[1];
         v3 x = vmuls(q, f[3]);
         float acc[3] = {0.0f, 0.0f, 0.0f};
-        for (int k = 0; k < 3; ++k) {
-            float amp = 1.0f, fr = 1.0f, sum = 0.0f;
-            for (uint32_t o = 0; o < oct; ++o) {
-                uint32_t sd = seed + (uint32_t)k * 0x9e3779b9u + o * 0x85ebca6bu;
-                CNT(noise_octaves);
-                sum = sum + amp * rrte_oracle_value_noise(x.x * fr, x.y * fr, x.z * fr, sd);
-                amp = amp * f[5];
-                fr = fr * 2.0f;
-            }
-            acc[k] = sum;
+        float amp = 1.0f, fr = 1.0f;
+        for (uint32_t o = 0; o < oct; ++o) {
+            float nv[3];
+            CNT(noise_octaves);
+            rrte_oracle_value_noise3(x.x * fr, x.y * fr, x.z * fr, seed + o * 0x85ebca6bu, nv);
+            for (int k = 0; k < 3; ++k) acc[k] = acc[k] + amp * nv[k];
+            amp = amp * f[5];
+            fr = fr * 2.0f;
         }
         q = V(q.x + f[4] * acc[0], q.y + f[4] * acc[1], q.z + f[4] * acc[2]);
         break;
@@ -1188,7 +1197,7 @@ double rrte_oracle_flops(const rrte_oracle_counts* c) {
     w_node[RRTE_SDF_SMOOTH_INTERSECTION] = 13;
     w_node[RRTE_SDF_BEND] = 39; w_node[RRTE_SDF_TWIST] = 39; w_node[RRTE_SDF_TAPER] = 16;
     w_node[RRTE_SDF_NOISE] = 15; w_node[RRTE_SDF_WAVE] = 35;
-    const double w_octave = 65.0;                     /* scale 3, value noise 58, accumulate 4 */
+    const double w_octave = 135.0; /* per octave: scale 3, cell 15, 24 corner values 48, 21 lerps 63, accumulate 6 */
     static const double w_light[4] = {29.0, 4.0, 39.0, 4.0};  /* point, directional, spot, ambient */
     const double w_shaded = 12.0, w_ndl = 5.0, w_shadow = 16.0, w_term = 10.0, w_ref_term = 8.0;
     static const double w_scatter[4] = {35.0, 50.0, 77.0, 0.0};  /* + 7 for the recursion combine */

@@ -57,7 +57,7 @@ typedef struct rrte_oracle_counts {
     uint64_t sdf_steps;          /* sphere-tracing steps (one program evaluation each)  */
     uint64_t sdf_normals;        /* tetrahedral normal estimates (4 evaluations each)  */
     uint64_t sdf_nodes[128];     /* program node evaluations by op (all evaluations)   */
-    uint64_t noise_octaves;      /* value-noise evaluations (3 per octave per NOISE node) */
+    uint64_t noise_octaves;      /* 3-channel value-noise evaluations (1 per octave per NOISE node) */
     uint64_t light_evals[4];     /* Light::illuminate by RRTE_LIGHT_* kind            */
     uint64_t shaded_hits;        /* hits with a material (base colour)                */
     uint64_t lambert_lights;     /* LAMBERT_SHADOW: N.L evaluations (non-ambient)     */
@@ -90,7 +90,7 @@ void rrte_oracle_mat4_srt(const float trs[10], float m_out[16]);
 void rrte_oracle_mat4_inverse(const float m[16], float inv_out[16]);
 float rrte_oracle_sinf(float x);
 float rrte_oracle_cosf(float x);
-float rrte_oracle_value_noise(float x, float y, float z, uint32_t seed);
+void rrte_oracle_value_noise3(float x, float y, float z, uint32_t seed, float out[3]);
 
 #ifdef __cplusplus
 }

@@ -442,29 +442,44 @@ __device__ __forceinline__ void sincos_rrte(float x, float& so, float& co) {
     co = (q == 0) ? c_ : (q == 1) ? -s_ : (q == 2) ? -c_ : s_;
 }
 
-__device__ __forceinline__ float lattice(int32_t ix, int32_t iy, int32_t iz, uint32_t seed) {
-    uint32_t h = seed ^ ((uint32_t)ix * 0x8da6b343u) ^ ((uint32_t)iy * 0xd8163841u) ^ ((uint32_t)iz * 0xcb1ab31fu);
+// Three-channel value noise (build-defined, DESIGN.md §6 'Deformers'; oracle rrte_oracle_value_noise3):
+// every lattice corner has ONE 32-bit hash of (seed, corner) whose bits give its three values in
+// [-1, 1) -- bits 0-10 and 11-21 (step 2^-10), bits 22-31 (step 2^-9) -- each channel interpolated
+// trilinearly with the smoothstep fade.  (Rounds 1-5 hashed each channel separately: three times the
+// integer work, ~45 % of the deformation-stress frame)
+// The corner's seed-independent part of the hash (xor is associative and commutative, so
+// seed ^ corner_key is the word seed ^ ix*A ^ iy*B ^ iz*C of the oracle in any grouping).
+__device__ __forceinline__ uint32_t corner_key(int32_t ix, int32_t iy, int32_t iz) {
+    return ((uint32_t)ix * 0x8da6b343u ^ (uint32_t)iy * 0xd8163841u) ^ (uint32_t)iz * 0xcb1ab31fu;
+}
+__device__ __forceinline__ uint32_t lattice_mix(uint32_t h) {
     h = (h ^ (h >> 16)) * 0x7feb352du;
     h = (h ^ (h >> 15)) * 0x846ca68bu;
-    h = h ^ (h >> 16);
-    return (float)(h >> 8) * 1.1920928955078125e-7f - 1.0f;
+    return h ^ (h >> 16);
 }
 __device__ __forceinline__ float lerpf_(float a, float b, float t) { return a + (b - a) * t; }
-__device__ __forceinline__ float value_noise(float x, float y, float z, uint32_t seed) {
+__device__ __forceinline__ void value_noise3(float x, float y, float z, uint32_t seed, float out[3]) {
     float fx0 = floorf(x), fy0 = floorf(y), fz0 = floorf(z);
     int32_t ix = (int32_t)fx0, iy = (int32_t)fy0, iz = (int32_t)fz0;
     float fx = x - fx0, fy = y - fy0, fz = z - fz0;
-    float ux = fx * fx * (3.0f - 2.0f * fx);
-    float uy = fy * fy * (3.0f - 2.0f * fy);
-    float uz = fz * fz * (3.0f - 2.0f * fz);
-    float c000 = lattice(ix, iy, iz, seed), c100 = lattice(ix + 1, iy, iz, seed);
-    float c010 = lattice(ix, iy + 1, iz, seed), c110 = lattice(ix + 1, iy + 1, iz, seed);
-    float c001 = lattice(ix, iy, iz + 1, seed), c101 = lattice(ix + 1, iy, iz + 1, seed);
-    float c011 = lattice(ix, iy + 1, iz + 1, seed), c111 = lattice(ix + 1, iy + 1, iz + 1, seed);
-    float x00 = lerpf_(c000, c100, ux), x10 = lerpf_(c010, c110, ux);
-    float x01 = lerpf_(c001, c101, ux), x11 = lerpf_(c011, c111, ux);
-    float y0 = lerpf_(x00, x10, uy), y1 = lerpf_(x01, x11, uy);
-    return lerpf_(y0, y1, uz);
+    const float ux = fx * fx * (3.0f - 2.0f * fx);
+    const float uy = fy * fy * (3.0f - 2.0f * fy);
+    const float uz = fz * fz * (3.0f - 2.0f * fz);
+    float v[3][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t h = lattice_mix(seed ^ corner_key(ix + (j & 1), iy + ((j >> 1) & 1), iz + ((j >> 2) & 1)));
+        v[0][j] = (float)(h & 0x7ffu) * 0x1p-10f - 1.0f;
+        v[1][j] = (float)((h >> 11) & 0x7ffu) * 0x1p-10f - 1.0f;
+        v[2][j] = (float)(h >> 22) * 0x1p-9f - 1.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float x00 = lerpf_(v[k][0], v[k][1], ux), x10 = lerpf_(v[k][2], v[k][3], ux);
+        float x01 = lerpf_(v[k][4], v[k][5], ux), x11 = lerpf_(v[k][6], v[k][7], ux);
+        float y0 = lerpf_(x00, x10, uy), y1 = lerpf_(x01, x11, uy);
+        out[k] = lerpf_(y0, y1, uz);
+    }
 }
 
 // ---------------------------------------------------------------- RNG

@@ -319,18 +319,21 @@ __device__ __forceinline__ f3 sdf_deform(G& g, uint32_t op, const uint32_t* __re
     case RRTE_SDF_NOISE: {
         uint32_t oct = iarg[0], seed = iarg[1];
         f3 x = vmuls(q, f[3]);
-        float acc[3];
+        // q += amplitude * sum_o persistence^o * noise3(x * 2^o, seed + o * 0x85ebca6b)
+        float acc[3] = {0.0f, 0.0f, 0.0f};
+#if defined(RRTE_ABLATE_NOISE)  // (timing only, wrong images: the noise deformer's cost, tools/stress_ab.sh)
+        (void)oct; (void)seed; (void)x;
+#else
+        float amp = 1.0f, fr = 1.0f;
+        for (uint32_t o = 0; o < oct; ++o) {
+            float nv[3];
+            value_noise3(x.x * fr, x.y * fr, x.z * fr, seed + o * 0x85ebca6bu, nv);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            float amp = 1.0f, fr = 1.0f, sum = 0.0f;
-            for (uint32_t o = 0; o < oct; ++o) {
-                uint32_t sd = seed + (uint32_t)k * 0x9e3779b9u + o * 0x85ebca6bu;
-                sum = sum + amp * value_noise(x.x * fr, x.y * fr, x.z * fr, sd);
-                amp = amp * f[5];
-                fr = fr * 2.0f;
-            }
-            acc[k] = sum;
+            for (int k = 0; k < 3; ++k) acc[k] = acc[k] + amp * nv[k];
+            amp = amp * f[5];
+            fr = fr * 2.0f;
         }
+#endif
         q = V(q.x + f[4] * acc[0], q.y + f[4] * acc[1], q.z + f[4] * acc[2]);
         break;
     }
@@ -2175,7 +2178,7 @@ __device__ __forceinline__ LaunchTile launch_tile(const KParams& kp) {
 // RRTE_DEBUG bit 2: the launch's derived indices, checked before any memory access that uses them.
 // Check-word bits: 1 list slot out of range, 2 decoded tile outside the launch's tiles, 4 frame index
 // >= nframes, 8 an output row outside the frame.
-__device__ __noinline__ bool launch_indices_ok(const KParams& kp, unsigned long long* counters) {
+__device__ __forceinline__ bool launch_indices_ok(const KParams& kp, unsigned long long* counters) {
     uint32_t bad = 0u;
     const uint32_t th = 64u >> kp.tile_shift, gy = (kp.rows + th - 1u) / th;
     const uint32_t k = blockIdx.z * kp.tiles_x + blockIdx.x;

@@ -500,27 +500,40 @@ def sincos(x):
     return so.astype(np.float32), co.astype(np.float32)
 
 
-def _lattice(ix, iy, iz, seed):
-    """Integer lattice hash -> [-1, 1): xor of per-axis multiplies, then a 32-bit finaliser."""
+def _lattice_hash(ix, iy, iz, seed):
+    """Integer lattice hash of one corner: xor of per-axis multiplies, then a 32-bit finaliser."""
     u = lambda a: a.astype(np.int64).astype(np.uint32)  # noqa: E731  two's complement wrap
     h = np.uint32(seed) ^ (u(ix) * np.uint32(0x8da6b343)) ^ (u(iy) * np.uint32(0xd8163841)) ^ (u(iz) * np.uint32(0xcb1ab31f))
     h = (h ^ (h >> np.uint32(16))) * np.uint32(0x7feb352d)
     h = (h ^ (h >> np.uint32(15))) * np.uint32(0x846ca68b)
-    h = h ^ (h >> np.uint32(16))
-    return (h >> np.uint32(8)).astype(np.float32) * F(1.1920928955078125e-7) - F(1)
+    return h ^ (h >> np.uint32(16))
 
 
-def value_noise(x, y, z, seed):
-    """Trilinear value noise over the integer lattice with the smoothstep fade 3t^2 - 2t^3."""
+def _channel(h, k):
+    """The corner's value of channel k in [-1, 1): bits 0-10 / 11-21 (step 2^-10), bits 22-31 (step 2^-9)."""
+    if k == 0:
+        return (h & np.uint32(0x7FF)).astype(np.float32) * F(2.0 ** -10) - F(1)
+    if k == 1:
+        return ((h >> np.uint32(11)) & np.uint32(0x7FF)).astype(np.float32) * F(2.0 ** -10) - F(1)
+    return (h >> np.uint32(22)).astype(np.float32) * F(2.0 ** -9) - F(1)
+
+
+def value_noise3(x, y, z, seed):
+    """Three-channel trilinear value noise (DESIGN.md §6 'Deformers'): ONE hash per lattice corner
+    gives that corner's three values; the smoothstep fade 3t^2 - 2t^3.  Returns [n0, n1, n2]."""
     fx0, fy0, fz0 = np.floor(x), np.floor(y), np.floor(z)
     ix, iy, iz = fx0.astype(np.int64), fy0.astype(np.int64), fz0.astype(np.int64)
     fx, fy, fz = x - fx0, y - fy0, z - fz0
     ux, uy, uz = (fx * fx * (F(3) - F(2) * fx), fy * fy * (F(3) - F(2) * fy), fz * fz * (F(3) - F(2) * fz))
-    L = lambda a, b, c: _lattice(ix + a, iy + b, iz + c, seed)  # noqa: E731
+    H = {(a, b, c): _lattice_hash(ix + a, iy + b, iz + c, seed) for a in (0, 1) for b in (0, 1) for c in (0, 1)}
     lerp = lambda a, b, t: a + (b - a) * t  # noqa: E731
-    x00, x10 = lerp(L(0, 0, 0), L(1, 0, 0), ux), lerp(L(0, 1, 0), L(1, 1, 0), ux)
-    x01, x11 = lerp(L(0, 0, 1), L(1, 0, 1), ux), lerp(L(0, 1, 1), L(1, 1, 1), ux)
-    return lerp(lerp(x00, x10, uy), lerp(x01, x11, uy), uz)
+    out = []
+    for k in range(3):
+        L = lambda a, b, c: _channel(H[(a, b, c)], k)  # noqa: E731
+        x00, x10 = lerp(L(0, 0, 0), L(1, 0, 0), ux), lerp(L(0, 1, 0), L(1, 1, 0), ux)
+        x01, x11 = lerp(L(0, 0, 1), L(1, 0, 1), ux), lerp(L(0, 1, 1), L(1, 1, 1), ux)
+        out.append(lerp(lerp(x00, x10, uy), lerp(x01, x11, uy), uz))
+    return out
 
 
 def deform(node, p):
@@ -544,15 +557,14 @@ def deform(node, p):
     elif op == abi.SDF_NOISE:  # q += amplitude * fbm3(frequency * q), `octaves`, `persistence`
         octaves, seed = ia[0], ia[1]
         x = [q[k] * f[3] for k in range(3)]
-        acc = []
-        for k in range(3):
-            amp, fr, tot = F(1), F(1), np.zeros_like(q[0])
-            for o in range(octaves):
-                sd = (seed + k * 0x9E3779B9 + o * 0x85EBCA6B) & 0xFFFFFFFF
-                tot = tot + amp * value_noise(x[0] * fr, x[1] * fr, x[2] * fr, sd)
-                amp = amp * f[5]
-                fr = fr * F(2)
-            acc.append(tot)
+        acc = [np.zeros_like(q[0]) for _ in range(3)]
+        amp, fr = F(1), F(1)
+        for o in range(octaves):
+            sd = (seed + o * 0x85EBCA6B) & 0xFFFFFFFF
+            nv = value_noise3(x[0] * fr, x[1] * fr, x[2] * fr, sd)
+            acc = [acc[k] + amp * nv[k] for k in range(3)]
+            amp = amp * f[5]
+            fr = fr * F(2)
         q = [q[k] + f[4] * acc[k] for k in range(3)]
     elif op == abi.SDF_WAVE:  # q[disp] += amplitude * sin(frequency * q[axis])
         ax, disp = ia[0], ia[1]

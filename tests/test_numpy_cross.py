@@ -82,8 +82,21 @@ def test_trig_and_noise_are_well_behaved():
     c = np.array([lib.rrte_oracle_cosf(float(x)) for x in xs])
     assert np.abs(s - np.sin(xs.astype(np.float64))).max() < 5e-7
     assert np.abs(c - np.cos(xs.astype(np.float64))).max() < 5e-7
-    v = np.array([lib.rrte_oracle_value_noise(float(x), 0.37, -1.3, 11) for x in np.linspace(-3, 3, 601)])
-    assert v.min() >= -1 and v.max() < 1 and np.abs(np.diff(v)).max() < 0.2
+    import ctypes as C
+    out = (C.c_float * 3)()
+    xs = np.linspace(-3, 3, 601, dtype=np.float32)
+    v = []
+    for x in xs:
+        lib.rrte_oracle_value_noise3(float(x), 0.37, -1.3, 11, out)
+        v.append(list(out))
+    v = np.array(v, dtype=np.float32)  # (601, 3): the three channels
+    assert v.min() >= -1 and v.max() < 1 and np.abs(np.diff(v, axis=0)).max() < 0.2
+    # the channels are distinct functions (one hash per corner, different bits of it)
+    assert min(np.abs(v[:, a] - v[:, b]).max() for a, b in ((0, 1), (0, 2), (1, 2))) > 0.1
+    # the numpy restatement gives the same bits
+    from numpy_ref import value_noise3
+    w = value_noise3(xs, np.full_like(xs, 0.37), np.full_like(xs, -1.3), 11)
+    assert np.array_equal(np.stack(w, 1).view(np.uint32), v.view(np.uint32))
 
 
 # ---------------------------------------------------------------- the SDF half

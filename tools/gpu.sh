@@ -4,7 +4,8 @@
 #   suite [PYTEST_K]      the -m gpu suite (optionally -k PYTEST_K)            -> gpurun_out/suite.log
 #   smoke                 __graft_entry__.smoke()                              -> gpurun_out/smoke.log
 #   bench NAME "ARGS"     python bench.py ARGS (one JSON line)                 -> gpurun_out/bench_NAME.log
-#   prof TAG              kernel trace + stats, the 20-step timeline, the PMC passes (tools/prof.sh)
+#   prof TAG "ARGS"       kernel trace + stats, the 20-step timeline, the PMC passes (tools/prof.sh) of
+#                         bench.py ARGS ("" = the headline)
 #   run NAME SECS "CMD"   any other command (a tool script), time-limited      -> gpurun_out/NAME.log
 # e.g.  gpurun --timeout 900 -- 'bash tools/gpu.sh suite smoke bench b20 "--steps 20 --warmup 5"'
 set -o pipefail
@@ -28,8 +29,8 @@ while [ $# -gt 0 ]; do
         || { tail -20 gpurun_out/bench_$name.log; echo "BENCH FAILED"; exit 1; }
       tail -1 gpurun_out/bench_$name.log | python3 tools/bench_summary.py ;;
     prof)
-      tag=$1; shift
-      bash tools/prof.sh "$tag" || { echo "PROF FAILED"; exit 1; } ;;
+      tag=$1; pargs=$2; shift 2
+      bash tools/prof.sh "$tag" "$pargs" || { echo "PROF FAILED"; exit 1; } ;;
     run)
       name=$1; secs=$2; cmd=$3; shift 3
       timeout -k 10 "$secs" bash -c "$cmd" > gpurun_out/$name.log 2>&1 || { tail -30 gpurun_out/$name.log; echo "RUN $name FAILED"; exit 1; }

@@ -55,6 +55,17 @@ out_md += ["## PMC counters (mean per ray_kernel dispatch, separate --pmc passes
 out_md += ["## derived", "", "```json", json.dumps({k: v for k, v in res.items() if k in ("hbm_bytes_per_launch",
                                                                                          "valu", "avg_kernel_ns")},
                                                   indent=1), "```", ""]
+# the driver's configuration traced (tools/prof.sh tl/: 5 warm-up frames, 20 sequential, 20 back to back,
+# then the 20 timed frames with 4 in flight): the timed frames' spans and overlap (tools/timeline2.py)
+tl = src / "tl" / "run_kernel_trace.csv"
+if tl.exists():
+    import subprocess
+    tmp = src / "timeline.md"
+    subprocess.run([sys.executable, str(Path(__file__).parent / "timeline2.py"), str(tl), "45", "20", str(tmp),
+                    "the driver's 20 timed steps (4 frames in flight)"], check=False, capture_output=True)
+    if tmp.exists():
+        out_md += ["## in-flight timeline of the timed frames (`rocprofv3 --kernel-trace`, tools/timeline2.py)", ""]
+        out_md += tmp.read_text().splitlines()[1:] + [""]
 Path("profiles").mkdir(exist_ok=True)
 Path(f"profiles/{name}.md").write_text("\n".join(out_md))
 Path(f"profiles/pmc_{name}.json").write_text(json.dumps(res, indent=1))
