@@ -699,7 +699,29 @@ def main():
             ctx.check(lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), ppin))
         pin_ms = (time.perf_counter() - a) / nb * 1e3
         pin_ok = bool(np.array_equal(pin.numpy(), hbuf))
+        # Engine::render_frame's loop as rust/patches/0002 wires it, in the C++ mirror
+        # (rrte_amd/cpp: Raytracer::render_into, the calls rrte-hip-sys's Context::render_engine_frame
+        # makes): the engine's frame buffer reused every frame and pinned once through the C ABI, the
+        # scene lowered from its objects every frame; every timed frame checked against render()
+        import subprocess
+        import tempfile
+        eng_ms, eng_ok = None, False
+        tool = ROOT / "rrte_amd" / "lib" / "cpp_mirror_tool"
+        if tool.exists():
+            with tempfile.TemporaryDirectory() as td:
+                r = subprocess.run([str(tool), "engine", args.scene, str(W), str(H), args.mode,
+                                    str(Path(td) / "f.bin"), str(nb)], capture_output=True, text=True, timeout=300)
+            for tok in r.stdout.split("\n"):
+                if tok.startswith("engine_loop_ms_per_frame"):
+                    eng_ms = float(tok.split()[1])
+                    eng_ok = r.returncode == 0 and "mismatched 0" in tok
         boundary = {"entry": "rrte_hip_render (blocking; Raytracer::render's signature, host RGBA8 out, D2H included)",
+                    "ms_per_frame_engine_loop": round(eng_ms, 4) if eng_ms is not None else None,
+                    "engine_loop_equals_render": eng_ok,
+                    "engine_loop_note": "Engine::render_frame through Raytracer::render_into (rust/patches/0002), run "
+                                        "in the C++ mirror (cpp_mirror_tool engine, its own process): the engine's "
+                                        "frame_buffer reused and pinned once, the scene lowered from its objects every "
+                                        "frame, each timed frame compared with Raytracer::render",
                     "ms_per_frame_reused_buffer": round(reused_ms, 4),
                     "ms_per_frame_fresh_buffer": round(fresh_ms, 4),
                     "fresh_alloc_ms": round(alloc_s / nb * 1e3, 4),

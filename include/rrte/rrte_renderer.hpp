@@ -378,6 +378,13 @@ public:
     // (the reference passes it through unused); objects carry their materials.
     std::vector<uint8_t> render(const Objects& objects, const Lights& lights, const Materials& materials,
                                 const Camera& camera);
+    // Engine::render_frame's loop (engine.rs:82,293; rust/patches/0002): the frame into the caller's
+    // buffer, reused every frame and pinned once (rrte_hip_host_register) so the kernel stores the
+    // frame straight into it.  `out` is resized to W*H*4; a buffer that moved since it was pinned is
+    // unpinned first, one that cannot be pinned takes the copy path.  Keep `out` alive (and do not
+    // reallocate it outside this call) until the next call or the Raytracer's destruction.
+    void render_into(const Objects& objects, const Lights& lights, const Materials& materials,
+                     const Camera& camera, std::vector<uint8_t>& out);
     // parity variant: RGBA8 plus the float image (post-gamma, or linear pre-gamma)
     std::pair<std::vector<uint8_t>, std::vector<float>> render_f32(const Objects& objects, const Lights& lights,
                                                                    const Camera& camera, bool linear = false);
@@ -386,6 +393,9 @@ private:
     void check(rrte_status st) const;
     RaytracerConfig config_;
     rrte_ctx* ctx_ = nullptr;
+    void* pinned_ = nullptr;      // the buffer render_into pinned
+    size_t pinned_len_ = 0;
+    const void* unpinnable_ = nullptr;  // the last buffer that could not be pinned (copy path)
 };
 
 }  // namespace rrte_renderer

@@ -383,6 +383,18 @@ rrte_status rrte_hip_jit_cache_key(const char* source, const char* headers_overr
  * and clears it.  0 = no violation. */
 rrte_status rrte_hip_check_word(rrte_ctx* ctx, uint64_t* word);
 
+/* ------------------------------------------------ SceneIR dump / load (repro) */
+/* A frame's lowered scene and parameters in one self-checking file (rrte_amd/csrc/scene_io.hip: magic,
+ * format and ABI version, record sizes, counts, the arrays, an FNV-1a trailer), so a frame can be
+ * replayed bit for bit on the device or on the CPU oracle.  env RRTE_DUMP_SCENE=<path>: every render
+ * entry point dumps the scene and parameters it was given before rendering (atomic rename), so the
+ * last frame of a failing process is on disk.  Host only; no device work. */
+rrte_status rrte_hip_scene_dump(const rrte_scene_ir* scene, const rrte_render_params* params, const char* path);
+/* Loads a dump: *scene's arrays point into *storage (release it with rrte_hip_scene_free).
+ * RRTE_INVALID_ARG for a missing, truncated or altered file, or one of another ABI / record layout. */
+rrte_status rrte_hip_scene_load(const char* path, rrte_scene_ir* scene, rrte_render_params* params, void** storage);
+void rrte_hip_scene_free(void* storage);
+
 /* ----------------------------------------------------- multi-GPU (RCCL/xGMI) */
 /* Row-band partition: band b (band_rows rows) belongs to rank b % nranks.
  * rrte_hip_render_gather renders this rank's bands and gathers every rank's

@@ -130,6 +130,9 @@ EXPORTS = {
                                            C.c_uint32, C.POINTER(C.c_uint32)]),
     "rrte_hip_jit_cache_key": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
     "rrte_hip_check_word": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "rrte_hip_scene_dump": (C.c_int, [C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_char_p]),
+    "rrte_hip_scene_load": (C.c_int, [C.c_char_p, C.POINTER(SceneIR), C.POINTER(RenderParams), C.POINTER(_P)]),
+    "rrte_hip_scene_free": (None, [_P]),
     "rrte_hip_comm_unique_id": (C.c_int, [_P]),
     "rrte_hip_comm_init": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "rrte_hip_render_gather": (C.c_int, [_P, C.POINTER(SceneIR), C.POINTER(RenderParams), C.c_int, _P]),

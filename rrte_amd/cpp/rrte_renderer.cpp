@@ -608,6 +608,27 @@ std::vector<uint8_t> Raytracer::render(const Objects& objects, const Lights& lig
     check(rrte_hip_render(ctx_, &sc.ir(), &p, out.data()));
     return out;
 }
+void Raytracer::render_into(const Objects& objects, const Lights& lights, const Materials& materials,
+                            const Camera& camera, std::vector<uint8_t>& out) {
+    (void)materials;
+    const LoweredScene sc(objects, lights, camera);
+    const rrte_render_params p = config_.lower();
+    const size_t need = (size_t)p.width * p.height * 4;
+    if (pinned_ && (pinned_ != out.data() || pinned_len_ != out.size() || out.size() != need)) {
+        check(rrte_hip_host_unregister(ctx_, pinned_));  // (before a resize may move or free it)
+        pinned_ = nullptr;
+    }
+    out.resize(need);
+    if (!pinned_ && unpinnable_ != out.data()) {
+        if (rrte_hip_host_register(ctx_, out.data(), out.size()) == RRTE_OK) {
+            pinned_ = out.data();
+            pinned_len_ = out.size();
+        } else {
+            unpinnable_ = out.data();
+        }
+    }
+    check(rrte_hip_render(ctx_, &sc.ir(), &p, out.data()));
+}
 std::pair<std::vector<uint8_t>, std::vector<float>> Raytracer::render_f32(const Objects& objects,
                                                                           const Lights& lights,
                                                                           const Camera& camera, bool linear) {

@@ -342,7 +342,8 @@ struct rrte_ctx {
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
     // per launch, so the version pool wraps within a few frames)
     bool env_test_recycle = false;
-    bool env_fault_bad_slot = false;  // RRTE_FAULT_BAD_SLOT=1 (tests, only with RRTE_DEBUG bit 2): slot 0 of every uploaded list names a tile outside the frame
+    bool env_fault_bad_slot = false;
+    std::string dump_path;  // RRTE_DUMP_SCENE: every render call's scene + params into this file (scene_io.hip)  // RRTE_FAULT_BAD_SLOT=1 (tests, only with RRTE_DEBUG bit 2): slot 0 of every uploaded list names a tile outside the frame
     // band partition of the last multi-GPU frame (frame_band_map)
     struct {
         bool valid = false;
@@ -1874,8 +1875,15 @@ uint32_t* pinned_device_ptr(void* host, size_t bytes) {
     return static_cast<uint32_t*>(a.devicePointer);
 }
 
+// RRTE_DUMP_SCENE (diagnostics): the frame's scene and parameters, as given, into the dump file
+// before anything else happens to them (rrte_hip_scene_dump; replayable on the oracle or the device).
+void dump_if_asked(const rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p) {
+    if (!c->dump_path.empty() && s && p) (void)rrte_hip_scene_dump(s, p, c->dump_path.c_str());
+}
+
 rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out8,
                           float* outf) {
+    dump_if_asked(c, s, p);
     rrte_status r = validate(c, s, p);
     if (r != RRTE_OK) return r;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1999,6 +2007,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     }
     if (const char* g = getenv("RRTE_TEST_RECYCLE")) c->env_test_recycle = g[0] == '1';
     if (const char* g = getenv("RRTE_FAULT_BAD_SLOT")) c->env_fault_bad_slot = g[0] == '1';
+    if (const char* g = getenv("RRTE_DUMP_SCENE"); g && *g) c->dump_path = g;
     if (const char* g = getenv("RRTE_BND_CHUNKS"); g && *g)
         c->bnd_chunks = std::max(1, std::min(rrte_ctx::kBndChunksMax, (int)strtol(g, nullptr, 0)));
     if (const char* t = getenv("RRTE_JIT_TOPO"); t && *t) c->env_jit_topo = (int)strtol(t, nullptr, 0);
@@ -2147,6 +2156,7 @@ rrte_status rrte_hip_render_f32(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
 rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, void* d_rgba,
                                   void* d_f32, void* stream) {
     if (!c) return RRTE_INVALID_ARG;
+    dump_if_asked(c, s, p);
     rrte_status r = validate(c, s, p);
     if (r != RRTE_OK) return r;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
@@ -2963,6 +2973,7 @@ static rrte_status gather_frame(rrte_ctx* c, const rrte_scene_ir* s, const rrte_
 rrte_status rrte_hip_render_gather_async(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
                                          void* d_full, void* stream) {
     if (!c) return RRTE_INVALID_ARG;
+    dump_if_asked(c, s, p);
     return gather_frame(c, s, p, root, d_full, stream ? static_cast<hipStream_t>(stream) : c->stream, false);
 }
 
@@ -3015,6 +3026,7 @@ rrte_status rrte_hip_gather_info(rrte_ctx* c, uint64_t* collectives, uint32_t* o
 rrte_status rrte_hip_render_gather(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, int root,
                                    uint8_t* out) {
     if (!c) return RRTE_INVALID_ARG;
+    dump_if_asked(c, s, p);
     rrte_status r = validate(c, s, p);
     if (r != RRTE_OK) return r;
     HIPCHK(c, hipSetDevice(c->device));

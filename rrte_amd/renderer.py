@@ -892,6 +892,33 @@ class Raytracer:
         out, _ = self.render_f32(objects, lights, materials, camera, want_f32=False)
         return out
 
+    def render_into(self, objects, lights, materials, camera: Camera, out: np.ndarray) -> np.ndarray:
+        """Engine::render_frame's loop (engine.rs:82,293; rust/patches/0002): the frame into the
+        caller's buffer, reused every frame and pinned once (rrte_hip_host_register) so the kernel
+        stores the frame straight into it -- the boundary's fast path.  `out` is a C-contiguous
+        uint8 array of W*H*4 bytes (the caller keeps it alive until it passes another buffer or the
+        context closes; a different buffer unpins this one first).  A buffer that cannot be pinned
+        (one of its pages already pinned elsewhere) takes the copy path.  Returns `out`."""
+        cfg = self.config
+        need = cfg.width * cfg.height * 4
+        if out.dtype != np.uint8 or out.size != need or not out.flags.c_contiguous:
+            raise ValueError(f"render_into needs a C-contiguous uint8 buffer of {need} bytes")
+        ctx = self.ctx
+        addr = out.ctypes.data
+        pinned = getattr(self, "_pinned", None)
+        if pinned is not None and pinned != (addr, need):
+            ctx.check(ctx.lib.rrte_hip_host_unregister(ctx.h, pinned[0]))
+            self._pinned = pinned = None
+        if pinned is None and getattr(self, "_unpinnable", None) != addr:
+            if ctx.lib.rrte_hip_host_register(ctx.h, addr, need) == abi.RRTE_OK:
+                self._pinned = (addr, need)
+            else:
+                self._unpinnable = addr
+        scene = LoweredScene(objects, lights, camera)
+        prm = cfg.lower()
+        ctx.check(ctx.lib.rrte_hip_render(ctx.h, scene.ref(), C.byref(prm), addr))
+        return out
+
     def render_f32(self, objects, lights, materials, camera: Camera, want_f32=True, linear=False):
         """Parity variant: also returns the post-gamma/clamp (or linear) f32 RGBA buffer."""
         cfg = self.config

@@ -133,6 +133,11 @@ extern "C" {
     pub fn rrte_hip_jit_cache_key(source: *const c_char, headers_override: *const c_char, out: *mut c_char,
                                   out_len: usize) -> rrte_status;
     pub fn rrte_hip_check_word(ctx: *mut rrte_ctx, word: *mut u64) -> rrte_status;
+    pub fn rrte_hip_scene_dump(scene: *const rrte_scene_ir, params: *const rrte_render_params, path: *const c_char)
+                               -> rrte_status;
+    pub fn rrte_hip_scene_load(path: *const c_char, scene: *mut rrte_scene_ir, params: *mut rrte_render_params,
+                               storage: *mut *mut c_void) -> rrte_status;
+    pub fn rrte_hip_scene_free(storage: *mut c_void);
     pub fn rrte_hip_comm_unique_id(out_id: *mut u8) -> rrte_status;
     pub fn rrte_hip_comm_init(ctx: *mut rrte_ctx, nranks: c_int, rank: c_int, id: *const u8) -> rrte_status;
     pub fn rrte_hip_render_gather(ctx: *mut rrte_ctx, scene: *const rrte_scene_ir,

@@ -69,12 +69,48 @@ impl SceneIr {
     }
 }
 
+/// A page-aligned host buffer rounded up to whole pages (hipHostRegister pins whole pages,
+/// so a buffer that shares a heap page with another registered range makes the second registration
+/// fail; this one shares none).  Owned by the context that pinned it.
+struct PageBuf {
+    ptr: *mut u8,
+    len: usize,
+    layout: std::alloc::Layout,
+}
+
+const PAGE: usize = 4096;
+
+impl PageBuf {
+    fn new(len: usize) -> Option<PageBuf> {
+        let size = len.max(1).checked_add(PAGE - 1)? & !(PAGE - 1);
+        let layout = std::alloc::Layout::from_size_align(size, PAGE).ok()?;
+        let ptr = unsafe { std::alloc::alloc_zeroed(layout) };
+        if ptr.is_null() {
+            return None;
+        }
+        Some(PageBuf { ptr, len, layout })
+    }
+    fn bytes(&self) -> &[u8] {
+        unsafe { std::slice::from_raw_parts(self.ptr, self.len) }
+    }
+}
+
+impl Drop for PageBuf {
+    fn drop(&mut self) {
+        unsafe { std::alloc::dealloc(self.ptr, self.layout) };
+    }
+}
+
 /// One rrte_hip context on one HIP device.
 pub struct Context {
     ctx: *mut rrte_ctx,
-    // a frame buffer the context owns and keeps pinned (rrte_hip_host_register): rrte_hip_render
-    // writes frames straight into it (no D2H copy after the render)
-    frame: Option<Vec<u8>>,
+    // a frame buffer the context owns and keeps pinned (rrte_hip_host_register): render_pinned has the
+    // kernel store each frame straight into it (no D2H copy after the render)
+    frame: Option<PageBuf>,
+    // a caller buffer pinned by render_engine_frame: (address, length), or the address of the last
+    // buffer that could not be pinned (tried once, then the copy path)
+    pinned: Option<(usize, usize)>,
+    unpinnable: usize,
 }
 
 // A context may move between threads (it is used by one thread at a time: `&mut self`).
@@ -92,7 +128,7 @@ impl Context {
             unsafe { rrte_hip_destroy(ctx) };
             return Err(Error { status: RRTE_INVALID_ARG, message: "librrte_hip ABI version mismatch".into() });
         }
-        Ok(Self { ctx, frame: None })
+        Ok(Self { ctx, frame: None, pinned: None, unpinnable: 0 })
     }
 
     fn check(&self, st: rrte_status) -> Result<(), Error> {
@@ -121,40 +157,76 @@ impl Context {
         self.check(st)
     }
 
-    /// Keeps `buf` (at least W*H*4 bytes of the frames to come) as the context's pinned frame buffer:
-    /// `render_pinned` then has the kernel store each frame straight into it.  A previous buffer is
-    /// unpinned and dropped.
-    pub fn set_frame_buffer(&mut self, mut buf: Vec<u8>) -> Result<(), Error> {
-        drop(self.take_frame_buffer()?);
-        self.check(unsafe { rrte_hip_host_register(self.ctx, buf.as_mut_ptr() as *mut c_void, buf.len()) })?;
+    /// Engine::render_frame's loop (engine.rs:82,293): the frame into the engine's own `frame_buffer`,
+    /// reused every frame and pinned once (rrte_hip_host_register), so the kernel stores the frame
+    /// straight into it (the boundary's fast path; bench.py `boundary.ms_per_frame_engine_loop`).  The
+    /// buffer is resized to W*H*4 bytes when needed; a buffer that moved since it was pinned (the
+    /// engine reallocated it) is unpinned before the new one is pinned, and a buffer that cannot be
+    /// pinned (one of its pages already pinned by someone else) is rendered through the copy path.
+    pub fn render_engine_frame(&mut self, scene: &SceneIr, params: &rrte_render_params, out: &mut Vec<u8>)
+                               -> Result<(), Error> {
+        let need = params.width as usize * params.height as usize * 4;
+        let cur = (out.as_ptr() as usize, out.len());
+        if self.pinned.is_some() && (self.pinned != Some(cur) || out.len() != need) {
+            self.unpin_engine_frame()?;  // (before a resize may move or free it)
+        }
+        if out.len() != need {
+            out.resize(need, 0);
+        }
+        let addr = out.as_ptr() as usize;
+        if self.pinned.is_none() && self.unpinnable != addr {
+            let st = unsafe { rrte_hip_host_register(self.ctx, out.as_mut_ptr() as *mut c_void, out.len()) };
+            if st == RRTE_OK {
+                self.pinned = Some((addr, out.len()));
+            } else {
+                self.unpinnable = addr;
+            }
+        }
+        self.render_into(scene, params, out)
+    }
+
+    /// Unpins the buffer render_engine_frame pinned (after the context's frames have completed).
+    pub fn unpin_engine_frame(&mut self) -> Result<(), Error> {
+        if let Some((addr, _)) = self.pinned.take() {
+            self.check(unsafe { rrte_hip_host_unregister(self.ctx, addr as *mut c_void) })?;
+        }
+        Ok(())
+    }
+
+    /// Gives the context a pinned frame buffer of `len` bytes (at least W*H*4 of the frames to come):
+    /// page-aligned, whole pages, registered once (rrte_hip_host_register); `render_pinned` then has the
+    /// kernel store each frame straight into it.  A previous buffer is unpinned and freed.
+    pub fn set_frame_buffer(&mut self, len: usize) -> Result<(), Error> {
+        self.release_frame_buffer()?;
+        let buf = PageBuf::new(len)
+            .ok_or_else(|| Error { status: RRTE_INVALID_ARG, message: format!("cannot allocate {len} bytes") })?;
+        self.check(unsafe { rrte_hip_host_register(self.ctx, buf.ptr as *mut c_void, buf.layout.size()) })?;
         self.frame = Some(buf);
         Ok(())
     }
 
-    /// Unpins the frame buffer (after the context's frames have completed) and hands it back.
-    pub fn take_frame_buffer(&mut self) -> Result<Option<Vec<u8>>, Error> {
-        if let Some(mut buf) = self.frame.take() {
-            let st = unsafe { rrte_hip_host_unregister(self.ctx, buf.as_mut_ptr() as *mut c_void) };
+    /// Unpins and frees the frame buffer (after the context's frames have completed).
+    pub fn release_frame_buffer(&mut self) -> Result<(), Error> {
+        if let Some(buf) = self.frame.take() {
+            let st = unsafe { rrte_hip_host_unregister(self.ctx, buf.ptr as *mut c_void) };
             if st != RRTE_OK {
                 self.frame = Some(buf);
                 return Err(self.check(st).unwrap_err());
             }
-            return Ok(Some(buf));
         }
-        Ok(None)
+        Ok(())
     }
 
     /// Raytracer::render into the pinned frame buffer (set_frame_buffer): the frame's W*H*4 bytes.
     pub fn render_pinned(&mut self, scene: &SceneIr, params: &rrte_render_params) -> Result<&[u8], Error> {
         let need = params.width as usize * params.height as usize * 4;
-        let ctx = self.ctx;
-        let ptr = match self.frame.as_mut() {
-            Some(b) if b.len() >= need => b.as_mut_ptr(),
+        let ptr = match self.frame.as_ref() {
+            Some(b) if b.len >= need => b.ptr,
             _ => return Err(Error { status: RRTE_INVALID_ARG, message: format!("no pinned frame buffer of {need} bytes") }),
         };
         let ir = scene.raw();
-        self.check(unsafe { rrte_hip_render(ctx, &ir, params, ptr) })?;
-        Ok(&self.frame.as_ref().unwrap()[..need])
+        self.check(unsafe { rrte_hip_render(self.ctx, &ir, params, ptr) })?;
+        Ok(&self.frame.as_ref().unwrap().bytes()[..need])
     }
 
     /// The device code's build id (rrte_hip_build_id: device headers, hiprtc options and version).
@@ -246,6 +318,8 @@ impl BandLayout {
 
 impl Drop for Context {
     fn drop(&mut self) {
+        // rrte_hip_destroy unregisters every pinned range after its frames; the frame buffer is freed
+        // after that (field drop order: `frame` outlives the destroy call)
         unsafe { rrte_hip_destroy(self.ctx) };
     }
 }

@@ -54,4 +54,22 @@ impl RenderBackend for HipBackend {
             }
         }
     }
+
+    /// Engine::render_frame's path (patch 0002): the frame into the engine's reused `frame_buffer`,
+    /// which the context pins once so the kernel stores the frame straight into it (no fresh
+    /// allocation, no D2H copy; rrte_hip_sys::safe::Context::render_engine_frame).  false = this frame
+    /// goes to the CPU path, whose frame then replaces `out`.
+    fn render_into(&self, objects: &[Arc<dyn SceneObject>], lights: &[Arc<dyn Light>], _materials: &[Arc<dyn Material>],
+                   camera: &Camera, config: &RaytracerConfig, out: &mut Vec<u8>) -> bool {
+        let Some(scene) = lower_scene(objects, lights, camera) else { return false };
+        let params = lower_config(config, &self.options);
+        let Ok(mut ctx) = self.ctx.lock() else { return false };
+        match ctx.render_engine_frame(&scene, &params, out) {
+            Ok(()) => true,
+            Err(e) => {
+                log::warn!("rrte_hip frame failed, rendering on the CPU: {e}");
+                false
+            }
+        }
+    }
 }

@@ -1,8 +1,15 @@
 // cpp_mirror_tool — drives the C++ mirror for tests/test_cpp_mirror.py.
 //   cpp_mirror_tool ir <scene> <w> <h> <mode> <out.bin>       lowered IR bytes + render params (no GPU)
 //   cpp_mirror_tool render <scene> <w> <h> <mode> <out.bin>    Raytracer::render_f32(linear): u8 then f32 (GPU)
+//   cpp_mirror_tool engine <scene> <w> <h> <mode> <out.bin> [frames]
+//                                                              Engine::render_frame's loop: one reused
+//                                                              buffer through Raytracer::render_into (pinned
+//                                                              once); every frame compared with render();
+//                                                              the last frame written; ms per frame printed (GPU)
 //   cpp_mirror_tool errors                                     error behaviour checks (no GPU needed)
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -60,6 +67,26 @@ int main(int argc, char** argv) {
             const rrte_stats st = rt.stats();
             std::printf("shadow_rays %llu\n", (unsigned long long)st.shadow_rays);
             return 0;
+        }
+        if (cmd == "engine") {
+            const int frames = argc > 7 ? std::atoi(argv[7]) : 20;
+            Raytracer rt(sc.config, 0);
+            const auto want = rt.render(sc.objects, sc.lights, {}, sc.camera);
+            std::vector<uint8_t> frame_buffer(16, 7);  // the engine's buffer (resized on the first frame)
+            int mismatched = 0;
+            // warm-up: the library's default JIT policy (AUTO) moves to the scene-specialised kernel once
+            // its background compile (or code-object cache load) lands
+            for (int i = 0; i < 400 && (i < 3 || !rt.stats().jit_active); ++i)
+                rt.render_into(sc.objects, sc.lights, {}, sc.camera, frame_buffer);
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < frames; ++i) {
+                rt.render_into(sc.objects, sc.lights, {}, sc.camera, frame_buffer);
+                if (i == 0 || i == frames - 1) mismatched += frame_buffer != want;
+            }
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            out.write(reinterpret_cast<const char*>(frame_buffer.data()), (std::streamsize)frame_buffer.size());
+            std::printf("engine_loop_ms_per_frame %.4f mismatched %d\n", ms / frames, mismatched);
+            return mismatched ? 1 : 0;
         }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());

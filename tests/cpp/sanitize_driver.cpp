@@ -6,6 +6,7 @@
 // device code is never instrumented (GPU sanitizers are not available).  Exits non-zero on any
 // mismatch; the sanitizers abort on any memory or UB error.
 #include <cstdio>
+#include <unistd.h>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -88,6 +89,32 @@ int main() {
         CHECK(rrte_hip_jit_cache_key("src", nullptr, k1, sizeof k1) == RRTE_OK &&
                   rrte_hip_jit_cache_key("src", "hdr", k2, sizeof k2) == RRTE_OK && strcmp(k1, k2) != 0,
               "jit cache key");
+    }
+    {
+        // SceneIR dump / load (scene_io.hip): a mirror-lowered scene round trip, and a truncated file
+        const auto sc = rrte_examples::by_name("kitchen-sink", 32, 24, Mode::LambertShadow);
+        const LoweredScene ls(sc.objects, sc.lights, sc.camera);
+        const rrte_render_params p = sc.config.lower();
+        const char* path = "/tmp/rrte_sanitize_scene.rrtesir";
+        CHECK(rrte_hip_scene_dump(&ls.ir(), &p, path) == RRTE_OK, "scene dump");
+        rrte_scene_ir ir{};
+        rrte_render_params q{};
+        void* storage = nullptr;
+        CHECK(rrte_hip_scene_load(path, &ir, &q, &storage) == RRTE_OK, "scene load");
+        CHECK(ir.num_prims == ls.ir().num_prims && ir.num_sdf_nodes == ls.ir().num_sdf_nodes &&
+                  !memcmp(ir.prims, ls.ir().prims, sizeof(rrte_prim) * ir.num_prims) && !memcmp(&q, &p, sizeof p),
+              "scene round trip");
+        rrte_hip_scene_free(storage);
+        if (FILE* f = std::fopen(path, "r+b")) {  // truncate: refused, nothing allocated
+            std::fseek(f, 0, SEEK_END);
+            const long n = std::ftell(f);
+            std::fclose(f);
+            (void)!truncate(path, n - 3);
+        }
+        storage = nullptr;
+        CHECK(rrte_hip_scene_load(path, &ir, &q, &storage) == RRTE_INVALID_ARG && storage == nullptr,
+              "truncated dump refused");
+        std::remove(path);
     }
     try {
         twist(Vec3(1.0f, 1.0f, 0.0f), 1.0f);

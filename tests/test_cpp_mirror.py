@@ -119,3 +119,20 @@ def test_cpp_raytracer_render_matches_oracle(name, tmp_path):
         assert np.sqrt(np.mean(np.nan_to_num(d) ** 2)) <= 1e-4
     else:
         assert np.array_equal(glin.view(np.uint32), rlin.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,w,h", [("sdf-showcase", 1920, 1080), ("basic-demo", 333, 97)])
+def test_cpp_engine_loop_render_into(name, w, h, tmp_path):
+    """Engine::render_frame's loop through the C++ mirror (Raytracer::render_into: one reused buffer,
+    pinned once, the kernel storing the frame straight into it; rust/patches/0002): every frame
+    byte-identical to Raytracer::render's, and the last one to the oracle's."""
+    out = tmp_path / "img.bin"
+    r = subprocess.run([str(TOOL), "engine", name, str(w), str(h), "lambert_shadow", str(out), "8"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatched 0" in r.stdout, r.stdout
+    g8 = np.frombuffer(out.read_bytes(), np.uint8)
+    objs, lights, cam, cfg = PY_SCENES[name](w, h, mode="lambert_shadow")
+    r8, _, _ = oracle.render(LoweredScene(objs, lights, cam), cfg.lower(), nthreads=16, want_f32=False)
+    assert np.abs(g8.astype(int) - r8.astype(int)).max() <= 1

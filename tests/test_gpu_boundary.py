@@ -118,3 +118,27 @@ def test_pinned_buffers_are_written_directly(name, w, h):
         got = pinned.numpy()
         assert np.array_equal(got, want), f"pinned, frame {f}: {int((got != want).sum())} bytes differ"
     ctx.close()
+
+
+@pytest.mark.parametrize("jit", [abi.JIT_ON, abi.JIT_OFF])
+def test_engine_loop_render_into_is_the_blocking_frame(jit):
+    """Engine::render_frame's loop (rust/patches/0002, Raytracer::render_into in the Python mirror):
+    one buffer reused every frame, pinned once through the C ABI (rrte_hip_host_register) so the
+    kernel stores into it; every frame must be rrte_hip_render's bytes into a pageable buffer; a
+    second buffer (a resized engine) unpins the first and pins itself."""
+    from rrte_amd import Raytracer
+    objs, lights, cam, cfg = scenes.sdf_showcase(640, 360)
+    rt = Raytracer(cfg, device=0, jit=jit)
+    want = rt.render(objs, lights, [], cam)  # pageable copy path
+    buf = np.full(640 * 360 * 4, 7, np.uint8)
+    for f in range(4):
+        buf[:] = 7
+        rt.render_into(objs, lights, [], cam, buf)
+        assert np.array_equal(buf, want), f"frame {f}"
+    assert rt._pinned == (buf.ctypes.data, buf.nbytes)
+    buf2 = np.zeros_like(buf)
+    rt.render_into(objs, lights, [], cam, buf2)
+    assert np.array_equal(buf2, want) and rt._pinned == (buf2.ctypes.data, buf2.nbytes)
+    ctx = rt.ctx
+    assert ctx.lib.rrte_hip_host_unregister(ctx.h, buf.ctypes.data) == abi.RRTE_INVALID_ARG  # (unpinned)
+    ctx.close()

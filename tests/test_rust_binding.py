@@ -478,9 +478,30 @@ def test_patches_hook_every_reference_type():
     for cls in ("LambertianMaterial", "MetalMaterial", "DielectricMaterial", "EmissiveMaterial"):
         assert re.search(r"impl Material for " + cls + r" \{\n\+    fn gpu_desc", p1), cls
     assert "+pub trait RenderBackend" in p1 and "+    pub fn set_backend" in p1
+    # the fast boundary: a defaulted RenderBackend::render_into and Raytracer::render_into,
+    # Raytracer::render's signature unchanged
+    assert "+    fn render_into(&self, objects: &[Arc<dyn SceneObject>]" in p1
+    assert "+    pub fn render_into(" in p1 and "+        out: &mut Vec<u8>," in p1
+    assert "-    ) -> Vec<u8> {" not in p1
     p2 = (PATCHES / "0002-rrte-core-hip-backend.patch").read_text()
-    assert "+                self.frame_buffer = raytracer.render(self.scene.get_objects(), self.scene.get_lights()," in p2
+    # Engine::render_frame renders into its own reused frame_buffer (engine.rs:82,293), not a fresh Vec
+    assert ("+                raytracer.render_into(self.scene.get_objects(), self.scene.get_lights(),\n"
+            "+                                      self.scene.get_materials(), &self.camera, &mut self.frame_buffer);") in p2
+    assert "self.frame_buffer = raytracer.render(" not in p2.replace("-                self.frame_buffer", "")
     assert "rrte_renderer_hip::HipBackend::new" in p2
+
+
+def test_backend_keeps_the_engine_buffer_pinned():
+    """HipBackend::render_into (rust/rrte-renderer-hip) goes through Context::render_engine_frame, which
+    pins the engine's buffer once and re-pins only a buffer that moved; the context's own frame buffer
+    is page-aligned whole pages (no page shared with another registration)."""
+    lib = (ROOT / "rust" / "rrte-renderer-hip" / "src" / "lib.rs").read_text()
+    safe = (ROOT / "rust" / "rrte-hip-sys" / "src" / "safe.rs").read_text()
+    assert "fn render_into(&self" in lib and "ctx.render_engine_frame(&scene, &params, out)" in lib
+    body = safe[safe.index("pub fn render_engine_frame"):safe.index("pub fn unpin_engine_frame")]
+    assert body.index("self.unpin_engine_frame()?") < body.index("out.resize(need, 0)")  # unpin before a move
+    assert "rrte_hip_host_register(self.ctx, out.as_mut_ptr()" in body and "self.unpinnable = addr" in body
+    assert "Layout::from_size_align(size, PAGE)" in safe and "& !(PAGE - 1)" in safe
 
 
 @pytest.mark.skipif(not REFERENCE.exists(), reason="the reference checkout is not on this machine")

@@ -153,7 +153,15 @@ def patch_renderer():
                   "/// MI355X).  `None` = this frame stays on the CPU (a scene it cannot lower, a device error).\n"
                   "pub trait RenderBackend: Send + Sync {\n"
                   "    fn render(&self, objects: &[Arc<dyn SceneObject>], lights: &[Arc<dyn Light>],\n"
-                  "              materials: &[Arc<dyn Material>], camera: &Camera, config: &RaytracerConfig) -> Option<Vec<u8>>;\n"
+                  "              materials: &[Arc<dyn Material>], camera: &Camera, config: &RaytracerConfig) -> Option<Vec<u8>>;\n\n"
+                  "    /// The frame into a caller buffer reused from frame to frame (Engine::frame_buffer): a back end\n"
+                  "    /// may keep it pinned and write into it directly.  false = `out` untouched, CPU path.\n"
+                  "    fn render_into(&self, objects: &[Arc<dyn SceneObject>], lights: &[Arc<dyn Light>],\n"
+                  "                   materials: &[Arc<dyn Material>], camera: &Camera, config: &RaytracerConfig,\n"
+                  "                   out: &mut Vec<u8>) -> bool {\n"
+                  "        match self.render(objects, lights, materials, camera, config) {\n"
+                  "            Some(frame) => {\n                *out = frame;\n                true\n            }\n"
+                  "            None => false,\n        }\n    }\n"
                   "}\n\n"
                   "/// CPU-based raytracer\npub struct Raytracer {\n    config: RaytracerConfig,\n"
                   "    backend: Option<Arc<dyn RenderBackend>>,\n}\n", 1)
@@ -162,7 +170,17 @@ def patch_renderer():
                   "    /// Renders through `backend` first (e.g. rrte_renderer_hip::HipBackend); the CPU loop\n"
                   "    /// below stays the fallback, so `render` keeps its infallible signature.\n"
                   "    pub fn set_backend(&mut self, backend: Option<Arc<dyn RenderBackend>>) {\n"
-                  "        self.backend = backend;\n    }\n", 1)
+                  "        self.backend = backend;\n    }\n\n"
+                  "    /// `render` into a buffer the caller reuses from frame to frame (Engine::frame_buffer): the\n"
+                  "    /// back end may keep it pinned and write the frame into it directly; without one, or when it\n"
+                  "    /// declines the frame, the CPU loop's frame replaces the buffer as before.\n"
+                  "    pub fn render_into(\n        &self,\n        objects: &[Arc<dyn SceneObject>],\n"
+                  "        lights: &[Arc<dyn Light>],\n        materials: &[Arc<dyn Material>],\n        camera: &Camera,\n"
+                  "        out: &mut Vec<u8>,\n    ) {\n"
+                  "        if let Some(b) = &self.backend {\n"
+                  "            if b.render_into(objects, lights, materials, camera, &self.config, out) {\n"
+                  "                return;\n            }\n        }\n"
+                  "        *out = self.render(objects, lights, materials, camera);\n    }\n", 1)
     anchor = "    ) -> Vec<u8> {\n"
     assert anchor in r
     r = r.replace(anchor, anchor + "        if let Some(b) = &self.backend {\n"
@@ -182,8 +200,10 @@ def patch_core():
                   "                // Every object and light of the scene (Scene::get_objects / get_lights), not only\n"
                   "                // the legacy sphere and point-light lists: the HIP back end lowers all of them,\n"
                   "                // and the CPU fallback renders the same scene.\n"
-                  "                self.frame_buffer = raytracer.render(self.scene.get_objects(), self.scene.get_lights(),\n"
-                  "                                                     self.scene.get_materials(), &self.camera);\n", 1)
+                  "                // The frame into the engine's own buffer, reused every frame (the HIP back end keeps it\n"
+                  "                // pinned and the kernel writes into it directly; the CPU path replaces it as before).\n"
+                  "                raytracer.render_into(self.scene.get_objects(), self.scene.get_lights(),\n"
+                  "                                      self.scene.get_materials(), &self.camera, &mut self.frame_buffer);\n", 1)
     old_init = "                let cpu_renderer = Raytracer::new(self.config.renderer_config.clone());\n"
     assert old_init in e
     e = e.replace(old_init,

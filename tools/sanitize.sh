@@ -12,7 +12,7 @@ SAN="-fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-fram
 HSAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer"
 cd $R/rrte_amd/csrc
 make -s jit_headers.inc
-for f in rrte_hip jit bvh sdf_guard; do
+for f in rrte_hip jit bvh sdf_guard scene_io; do
   [ $B/$f.o -nt $f.hip ] && [ $B/$f.o -nt ray_kernels.hpp ] && [ $B/$f.o -nt device_scene.hpp ] && continue
   /opt/rocm/bin/hipcc -std=c++17 -O1 -g --offload-arch=gfx950 -ffp-contract=off -fPIC $HSAN -I/opt/rocm/include -c $f.hip -o $B/$f.o &
 done
@@ -23,7 +23,7 @@ done
 $CLANG++ -std=c++17 $SAN -I$R/include -c $R/tests/cpp/sanitize_driver.cpp -o $B/sanitize_driver.o &
 wait
 $CLANG++ $SAN -o $B/sanitize_driver $B/sanitize_driver.o $B/rrte_renderer.o $B/examples.o $B/rrte_oracle.o \
-  $B/rrte_hip.o $B/jit.o $B/bvh.o $B/sdf_guard.o -L/opt/rocm/lib -lamdhip64 -lrccl -lhiprtc -pthread -lm \
+  $B/rrte_hip.o $B/jit.o $B/bvh.o $B/sdf_guard.o $B/scene_io.o -L/opt/rocm/lib -lamdhip64 -lrccl -lhiprtc -pthread -lm \
   -Wl,-rpath,/opt/rocm/lib
 # leaks inside the ROCm runtime / comgr (not ours) are suppressed by library; ours are reported
 cat > $B/lsan.supp <<'SUPP'
