@@ -705,7 +705,7 @@ def main():
         # scene lowered from its objects every frame; every timed frame checked against render()
         import subprocess
         import tempfile
-        eng_ms, eng_ok = None, False
+        eng_ms, eng_ok, eng_lower_ms = None, False, None
         tool = ROOT / "rrte_amd" / "lib" / "cpp_mirror_tool"
         if tool.exists():
             with tempfile.TemporaryDirectory() as td:
@@ -714,10 +714,12 @@ def main():
             for tok in r.stdout.split("\n"):
                 if tok.startswith("engine_loop_ms_per_frame"):
                     eng_ms = float(tok.split()[1])
+                    eng_lower_ms = float(tok.split()[5])
                     eng_ok = r.returncode == 0 and "mismatched 0" in tok
         boundary = {"entry": "rrte_hip_render (blocking; Raytracer::render's signature, host RGBA8 out, D2H included)",
                     "ms_per_frame_engine_loop": round(eng_ms, 4) if eng_ms is not None else None,
                     "engine_loop_equals_render": eng_ok,
+                    "engine_loop_lowering_ms": eng_lower_ms,
                     "engine_loop_note": "Engine::render_frame through Raytracer::render_into (rust/patches/0002), run "
                                         "in the C++ mirror (cpp_mirror_tool engine, its own process): the engine's "
                                         "frame_buffer reused and pinned once, the scene lowered from its objects every "
