@@ -433,6 +433,7 @@ __device__ __forceinline__ bool sdf_guard(G& gp, uint32_t gop, const float* gf, 
 template <uint32_t F = kFeatAll>
 struct SdfProgramT {
     static constexpr bool kSmall = false;
+    static constexpr int kPlan = 0;  // (sdf_parts_plan: no part-wise secant exit)
     const rrte_sdf_node* __restrict__ nodes;
     uint32_t count;
     template <class G>
@@ -497,6 +498,7 @@ using SdfProgram = SdfProgramT<kFeatAll>;
 template <uint32_t OP>
 struct SdfLeafProgram {
     static constexpr bool kSmall = true;
+    static constexpr int kPlan = 0;  // (sdf_parts_plan: no part-wise secant exit)
     NodeArgs a;  // the node's arguments (load_uniform)
     __device__ __forceinline__ float leaf_scale() const {
         float k = 0.0f;
@@ -617,6 +619,7 @@ template <class S, uint32_t FIRST, uint32_t COUNT>
 struct SdfStaticProgram {
     const S& sc;
     static constexpr bool kSmall = COUNT <= 8u;
+    static constexpr int kPlan = 0;
     // the secant exit's leaf scale (sdf_leaf_scale): folded for a full scene, the host's value in the
     // program's first node's spare slot f[11] for a topology scene (rrte_hip.hip upload_scene)
     __device__ __forceinline__ float leaf_scale() const {
@@ -634,6 +637,79 @@ struct SdfStaticProgram {
         uint32_t sp = 0, pp = 0;
         sdf_static_range<S, FIRST, 0u, COUNT, true>(sc, g, vs, ps, sp, pp, p);
         return vs[0];
+    }
+    __device__ __forceinline__ float operator()(f3 p) const {
+        GuardNow g;
+        return eval(p, g);
+    }
+};
+
+// Part-wise secant early miss (round 6): two convex 1-Lipschitz leaves under one CSG op whose result is
+// bounded below by its parts.  f = min(a, b) (union) >= the smaller part; the smooth union
+// smin(a, b, k) = a h + b (1 - h) - k h (1 - h) >= min(a, b) - k/4 for every h in [0, 1] (so whatever
+// h the rounding produced); the difference max(a, -b) >= a; the smooth difference -smin(-a, b, k) >=
+// max(a, -b) >= a (smin <= min; with the computed h within rounding of the exact one).  So once every
+// needed part is proven to stay >= E t (+ k/4 for the smooth union) by the convex secant argument of
+// sdf_march, no later step can hit.  Plans: 2 = both parts (union, smooth union), 3 = the left part
+// (difference, smooth difference); 0 = none.  Three-node programs of a full scene-specialised kernel
+// only (leaf, leaf, op, no CSG guard: guards need operands of >= 2 leaves); intersections of convex
+// leaves are convex as a whole (sdf_convex, plan 1 there).
+constexpr bool leaf_node_convex(const rrte_sdf_node& n) {
+    return n.op == RRTE_SDF_SPHERE || n.op == RRTE_SDF_BOX || n.op == RRTE_SDF_CYLINDER || n.op == RRTE_SDF_PRISM ||
+           n.op == RRTE_SDF_CAPSULE || (n.op == RRTE_SDF_CONE && n.f[3] > 0.0f && n.f[4] > 0.0f);
+}
+constexpr int sdf_parts_plan(const rrte_sdf_node* n, uint32_t count) {
+    if (count != 3u || n[0].op >= 32u || n[1].op >= 32u || n[2].op < 32u || n[2].op >= 64u) return 0;
+    if (n[0].i[2] != 0u || n[1].i[2] != 0u || n[2].i[2] != 0u) return 0;
+    const uint32_t op = n[2].op;
+    const bool smooth_ok = n[2].f[0] > 0.0f;
+    if ((op == RRTE_SDF_UNION || (op == RRTE_SDF_SMOOTH_UNION && smooth_ok)) && leaf_node_convex(n[0]) &&
+        leaf_node_convex(n[1]))
+        return 2;
+    if ((op == RRTE_SDF_DIFFERENCE || (op == RRTE_SDF_SMOOTH_DIFFERENCE && smooth_ok)) && leaf_node_convex(n[0]))
+        return 3;
+    return 0;
+}
+// Measured (tools/policy_ab.sh, two interleaved rounds, the headline): exact, a lone launch ~2 % shorter
+// (0.1022-0.1044 -> 0.1003-0.1024 ms), but the frame stream ~3 % slower (20 steps 0.0670-0.0675 ->
+// 0.0687-0.0696 ms, 200 steps 0.0626-0.0627 -> 0.0647-0.0654): the per-part tests on every step cost
+// more issue slots than the shortened marches save (profiles/r06_parts_exit_ab.log).  Off by default;
+// tests/test_gpu_parity.py keeps it exact (-DRRTE_PARTS_EXIT=1 against the plain march).
+#ifndef RRTE_PARTS_EXIT
+#define RRTE_PARTS_EXIT 0  // the part-wise secant exit (A/B switch)
+#endif
+
+// A full scene's three-node program (leaf A, leaf B, op) with a part-wise plan: the same operations in
+// the same order as the stack machine (sdf_node_step), plus the parts' values for the march's test.
+template <class S, uint32_t FIRST>
+struct SdfPartsProgram {
+    const S& sc;
+    static constexpr bool kSmall = true;
+    static constexpr int kPlan = sdf_parts_plan(S::nodes + FIRST, 3u);
+    static constexpr uint32_t kOp = S::nodes[FIRST + 2].op;
+    // extra margin of the parts' test: the smooth ops' rounding (<= D, see sdf_march) and the smooth
+    // union's k/4
+    static constexpr bool kSmooth = kOp == RRTE_SDF_SMOOTH_UNION || kOp == RRTE_SDF_SMOOTH_DIFFERENCE;
+    static constexpr float kQuarterK = kOp == RRTE_SDF_SMOOTH_UNION ? S::nodes[FIRST + 2].f[0] * 0.25f : 0.0f;
+    __device__ __forceinline__ float leaf_scale() const {
+        constexpr float k = sdf_leaf_scale(S::nodes + FIRST, 3u);
+        return k;
+    }
+    template <class G>
+    __device__ __forceinline__ float eval_parts(f3 p, G& g, float& a, float& b) const {
+        constexpr rrte_sdf_node na = S::nodes[FIRST], nb = S::nodes[FIRST + 1], no = S::nodes[FIRST + 2];
+        a = sdf_leaf(g, na.op, na.f, p);
+        b = sdf_leaf(g, nb.op, nb.f, p);
+        const float k = no.f[0];
+        if constexpr (kOp == RRTE_SDF_UNION) return smn(a, b);
+        else if constexpr (kOp == RRTE_SDF_DIFFERENCE) return smx(a, -b);
+        else if constexpr (kOp == RRTE_SDF_SMOOTH_UNION) return smin(g, a, b, k);
+        else return -smin(g, -a, b, k);  // RRTE_SDF_SMOOTH_DIFFERENCE
+    }
+    template <class G>
+    __device__ __forceinline__ float eval(f3 p, G& g) const {
+        float a, b;
+        return eval_parts(p, g, a, b);
     }
     __device__ __forceinline__ float operator()(f3 p) const {
         GuardNow g;
@@ -807,6 +883,36 @@ __device__ __forceinline__ bool sdf_march(const DPrim& pr, const EVAL& eval, con
     // t sequence and result as "if (d < eps*t) hit; t += d*scale; if (t > tend) miss" (NaN
     // included).  (A fully predicated form with a wave-uniform exit was measured slower.)
     bool hit = false;
+    if constexpr (EVAL::kPlan >= 2 && RRTE_PARTS_EXIT && !RRTE_MARCH_PAIR && !RRTE_DEFER_GUARDS) {
+        // part-wise secant early miss (SdfPartsProgram): every needed part proven to stay above
+        // E t + margin by its own secant; D as below (the parts are leaves of the same program)
+        const float E = eps * (1.0f + 0x1p-20f);
+        const float K = eval.leaf_scale();
+        const float D = 0x1p-17f * ((((fabsf(r.o.x) + fabsf(r.o.y)) + fabsf(r.o.z)) + tend) +
+                                    ((((fabsf(bc.x) + fabsf(bc.y)) + fabsf(bc.z)) + 4.0f * br) + K));
+        const float D3 = 3.0f * D;
+        const float D3M = EVAL::kSmooth ? (D3 + D) + EVAL::kQuarterK : D3;
+        float ap = __builtin_nanf(""), bp = __builtin_nanf(""), tp = t;
+RRTE_UNROLL_(RRTE_MARCH_UNROLL)
+        for (uint32_t i = 0; i < steps; ++i) {
+            f3 p = ray_at(r, t);
+            GuardNow g;
+            float a, b;
+            float d = eval.eval_parts(p, g, a, b);
+            hit = d < eps * t;
+            const float tn = t + d * scale;
+            bool safe = (a - E * t >= D3M) && ((a - ap) - E * (t - tp) >= D3);
+            if constexpr (EVAL::kPlan == 2) safe = safe && (b - E * t >= D3M) && ((b - bp) - E * (t - tp) >= D3);
+            const bool stop = hit || tn > tend || safe;
+            ap = a;
+            bp = b;
+            tp = t;
+            t = hit ? t : tn;
+            if (stop) break;
+        }
+        t_hit = t;
+        return hit;
+    }
     if constexpr (CONVEX) {
         const float E = eps * (1.0f + 0x1p-20f);
         const float K = eval.leaf_scale();
@@ -1384,6 +1490,17 @@ constexpr bool prim_convex() {
     if constexpr (S::kTopo) return S::topo_prims[I].convex;
     else return sdf_convex(S::nodes + S::prims[I].sdf_first, S::prims[I].sdf_count);
 }
+// Part-wise secant plan of object I (sdf_parts_plan): full scenes only (a topology kernel keeps the
+// whole-program convexity its host computed), and only with the default march loops.
+template <class S, uint32_t I>
+constexpr int prim_parts_plan() {
+    if constexpr (S::kTopo || !RRTE_PARTS_EXIT || RRTE_MARCH_PAIR || RRTE_MARCH_PRED != 0 || RRTE_DEFER_GUARDS)
+        return 0;
+    else if constexpr (S::prims[I].kind != RRTE_PRIM_SDF || S::prims[I].sdf_count != 3u)
+        return 0;
+    else
+        return sdf_parts_plan(S::nodes + S::prims[I].sdf_first, 3u);
+}
 template <bool NEED_HIT, class S, uint32_t I, bool ANY = false>
 __device__ __forceinline__ bool intersect_at(const S& sc, UC<I> ii, const Ray& r, float t_min, float t_max, Hit& out) {
     const DPrim pr = prim_at(sc, ii);
@@ -1395,6 +1512,9 @@ __device__ __forceinline__ bool intersect_at(const S& sc, UC<I> ii, const Ray& r
     else if constexpr (kind == RRTE_PRIM_CYLINDER) return isect_cylinder<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_CONE) return isect_cone<NEED_HIT>(pr, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_CAPSULE) return isect_capsule<NEED_HIT>(pr, r, t_min, t_max, out);
+    else if constexpr (kind == RRTE_PRIM_SDF && prim_parts_plan<S, I>() >= 2 && (ANY ? kSecantExit >= 1 : kSecantExit >= 2))
+        return isect_sdf<NEED_HIT, SdfPartsProgram<S, prim_first<S, I>()>, ANY, false>(
+            pr, SdfPartsProgram<S, prim_first<S, I>()>{sc}, r, t_min, t_max, out);
     else if constexpr (kind == RRTE_PRIM_SDF)
         return isect_sdf<NEED_HIT, SdfStaticProgram<S, prim_first<S, I>(), prim_count<S, I>()>, ANY,
                          (ANY ? kSecantExit >= 1 : kSecantExit >= 2) && prim_convex<S, I>()>(

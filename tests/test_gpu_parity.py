@@ -132,25 +132,31 @@ def test_shadow_culling_is_exact(case, jit, monkeypatch):
     assert out["0"][1] == out["1"][1]
 
 
+@pytest.mark.parametrize("scene", ["convex", "csg_parts"])
 @pytest.mark.parametrize("size", [(240, 160), (641, 359)])
-def test_convex_secant_early_miss_is_exact(size, monkeypatch):
+def test_convex_secant_early_miss_is_exact(size, scene, monkeypatch):
     """Scene-specialised any-hit marches of convex SDF objects stop once the secant bound proves
-    that no later step can hit (ray_kernels.hpp sdf_march CONVEX).  Exact: the image and the
-    shadow-ray count match the oracle bit for bit, and match the same kernel compiled without the
-    early miss (RRTE_JIT_EXTRA_OPTS=-DRRTE_SECANT_EXIT=0), with grazing and near-horizon lights,
-    degenerate convex sizes and non-convex controls."""
-    objs, lights, cam, cfg = se.convex_sdf_scene(*size)
+    that no later step can hit (ray_kernels.hpp sdf_march CONVEX), and those of two-leaf CSG objects
+    once every part their value is bounded by is proven (sdf_parts_plan, round 6).  Exact: the image
+    and the shadow-ray count match the oracle bit for bit, and match the same kernel compiled without
+    the early misses (RRTE_JIT_EXTRA_OPTS=-DRRTE_SECANT_EXIT=0), with grazing and near-horizon lights,
+    degenerate sizes and controls the exits must leave alone."""
+    fn = se.convex_sdf_scene if scene == "convex" else se.csg_parts_scene
+    objs, lights, cam, cfg = fn(*size)
     compare(objs, lights, cam, cfg, jit=abi.JIT_ON)
     out = {}
-    for opt in ("", "-DRRTE_SECANT_EXIT=0"):
+    # (the part-wise exit is an off-by-default switch: -DRRTE_PARTS_EXIT=1 checks it)
+    opts = ("", "-DRRTE_PARTS_EXIT=1", "-DRRTE_SECANT_EXIT=0")
+    for opt in opts:
         monkeypatch.setenv("RRTE_JIT_EXTRA_OPTS", opt)
         rt = Raytracer(cfg, device=0, jit=abi.JIT_ON)
         _, lin = rt.render_f32(objs, lights, [], cam, linear=True)
         st = rt.stats()
         assert st.jit_active == 1
         out[opt] = (lin.view(np.uint32).copy(), int(st.shadow_rays))
-    assert np.array_equal(out[""][0], out["-DRRTE_SECANT_EXIT=0"][0])
-    assert out[""][1] == out["-DRRTE_SECANT_EXIT=0"][1]
+    for opt in opts[:2]:
+        assert np.array_equal(out[opt][0], out["-DRRTE_SECANT_EXIT=0"][0]), opt
+        assert out[opt][1] == out["-DRRTE_SECANT_EXIT=0"][1], opt
 
 
 @pytest.mark.parametrize("jit", [abi.JIT_OFF, abi.JIT_ON])
