@@ -389,6 +389,10 @@ public:
     std::pair<std::vector<uint8_t>, std::vector<float>> render_f32(const Objects& objects, const Lights& lights,
                                                                    const Camera& camera, bool linear = false);
     rrte_stats stats() const;
+    // the C ABI call on an already lowered scene (diagnostics, tests/cpp/cpp_mirror_tool.cpp)
+    void render_raw(const rrte_scene_ir& ir, const rrte_render_params& p, uint8_t* out) {
+        check(rrte_hip_render(ctx_, &ir, &p, out));
+    }
 private:
     void check(rrte_status st) const;
     RaytracerConfig config_;

@@ -91,8 +91,16 @@ int main(int argc, char** argv) {
             size_t sink = 0;
             for (int i = 0; i < frames; ++i) sink += LoweredScene(sc.objects, sc.lights, sc.camera).ir().num_prims;
             const double lms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - l0).count();
-            std::printf("engine_loop_ms_per_frame %.4f mismatched %d lower_ms_per_frame %.4f (%zu)\n", ms / frames,
-                        mismatched, lms / frames, sink);
+            // diagnostics: the same frames through the C ABI with the scene lowered once
+            const LoweredScene once(sc.objects, sc.lights, sc.camera);
+            const rrte_render_params prm = sc.config.lower();
+            const auto c0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < frames; ++i) rt.render_raw(once.ir(), prm, frame_buffer.data());
+            const double cms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
+            std::printf("abi_same_buffer_ms_per_frame %.4f\n", cms / frames);
+            const rrte_stats est = rt.stats();
+            std::printf("engine_loop_ms_per_frame %.4f mismatched %d lower_ms_per_frame %.4f (%zu) jit %u kernel_ms %.4f\n",
+                        ms / frames, mismatched, lms / frames, sink, est.jit_active, est.kernel_ms);
             return mismatched ? 1 : 0;
         }
     } catch (const std::exception& e) {
