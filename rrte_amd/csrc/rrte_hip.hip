@@ -321,7 +321,10 @@ struct rrte_ctx {
     };
     // One tile-order state per launch shape that alternates within a frame: slot 0 for whole frames
     // and rank shares, slot 1 + i for row chunk i of a blocking frame (render_chunked)
-    static constexpr int kBndChunksMax = 8, kProfSlots = 1 + kBndChunksMax;
+    // tile-profile slots: 0 frames into device buffers and the copy path, 1..kBndChunksMax the row
+    // chunks of render_chunked, kZcProf zero-copy frames (their 32x2 tiles are another launch shape:
+    // an engine alternating copy-path and zero-copy frames must not re-profile every frame)
+    static constexpr int kBndChunksMax = 8, kZcProf = 1 + kBndChunksMax, kProfSlots = 2 + kBndChunksMax;
     TileProfile tprof[kProfSlots];
     // Blocking drop-in path (rrte_hip_render into a host buffer): the frame renders as row chunks on
     // streams of their own, and each chunk's D2H starts as soon as that chunk is done (render_chunked)
@@ -1537,6 +1540,7 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
         if (v != tp.cur && retired_done(tp.ret[v])) pick = v;
     }
     if (pick < 0) return false;
+    trace_rec(c, "hot-list upload: begin", nullptr, nullptr, (uint32_t)pick);
     tp.ret[pick].nev = 0;
     const size_t n = tp.slots.size(), stride = hot_stride((uint32_t)n);
     const size_t words = 8u * stride;  // XCD-major (KParams::hot_stride)
@@ -1548,7 +1552,9 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
         if (hipMalloc(reinterpret_cast<void**>(&tp.d_list[pick]), bytes) != hipSuccess) return false;
         tp.cap_list[pick] = words;
     }
+    trace_rec(c, "hot-list upload: device buffer", nullptr, nullptr, (uint32_t)pick);
     if (!reserve_hot_lists(tp, words)) return false;
+    trace_rec(c, "hot-list upload: reserved", nullptr, nullptr, (uint32_t)pick);
     if (tp.cap_h_list[pick] < words) return false;  // (reserve_hot_lists could not grow it yet)
     uint32_t* stage = tp.h_list[pick];
     for (size_t k = 0; k < n; ++k) stage[(k & 7u) * stride + (k >> 3)] = tp.slots[k];
@@ -1584,6 +1590,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
     key.append(reinterpret_cast<const char*>(shape), sizeof shape);
     const uint32_t tiles = L.gx * L.gy;
     if (tp.pending && hipEventQuery(tp.ev) == hipSuccess) {
+        trace_rec(c, "tile plan: profile landed", st, nullptr);
         tp.pending = false;
         if (tp.pending_key == key) {
             // the order is composed on a worker thread from a copy of the durations: a whole frame's
@@ -1599,6 +1606,7 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         }
     }
     if (tp.working && tp.work.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
+        trace_rec(c, "tile plan: worker result", st, nullptr);
         TilePlanResult r = tp.work.get();
         tp.working = false;
         if (r.key == key && r.slots.size() == tiles) {  // (a result for another shape is dropped)
@@ -1651,7 +1659,9 @@ bool plan_tile_order(rrte_ctx* c, LaunchPlan& L, const void* kern, hipStream_t s
         tp.cap_h = tiles;
     }
     if (!tp.ev && hipEventCreateWithFlags(&tp.ev, hipEventDisableTiming) != hipSuccess) return false;
+    trace_rec(c, "tile profile: reserve lists", st, nullptr, tiles);
     if (!reserve_hot_lists(tp, 8u * (size_t)hot_stride(tiles))) return false;
+    trace_rec(c, "tile profile: reserved", st, nullptr, tiles);
     k.tile_cost = tp.d_cost;  // every tile of frame 0 stores its duration (no clearing needed)
     tp.cam_sig = cam;
     tp.pending_key = key;
@@ -1906,7 +1916,7 @@ rrte_status render_common(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render
         HIPCHK(c, hipEventRecord(c->ev0, c->stream));
         if (zc) c->tile_shift = c->zc_tile_shift;  // whole 128-B lines per wave across PCIe
         r = launch(c, s, p, p->height, zc ? zc : c->d_rgba, outf ? c->d_f32 : nullptr, c->stream,
-                   zc && c->env_zc_system_store ? kFlagHostStore : 0u);
+                   zc && c->env_zc_system_store ? kFlagHostStore : 0u, 0u, zc ? rrte_ctx::kZcProf : 0);
         c->tile_shift = 3;
         if (r == RRTE_OK) r = hipEventRecord(c->ev1, c->stream) == hipSuccess ? RRTE_OK : RRTE_HIP_ERROR;
     }

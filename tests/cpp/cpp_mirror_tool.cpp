@@ -77,7 +77,9 @@ int main(int argc, char** argv) {
             int mismatched = 0;
             // warm-up: the library's default JIT policy (AUTO) moves to the scene-specialised kernel once
             // its background compile (or code-object cache load) lands
-            for (int i = 0; i < 400 && (i < 3 || !rt.stats().jit_active); ++i)
+            // (and past the launch shape's first frames: its tile profile, the worker's slowest-first list
+            // and that list's first upload -- one-time work of a new shape)
+            for (int i = 0; i < 400 && (i < 20 || !rt.stats().jit_active); ++i)
                 rt.render_into(sc.objects, sc.lights, {}, sc.camera, frame_buffer);
             mismatched += frame_buffer != want;  // (the last warm-up frame; the compares stay out of the timing)
             std::fill(frame_buffer.begin(), frame_buffer.end(), (uint8_t)7);
@@ -85,6 +87,9 @@ int main(int argc, char** argv) {
             for (int i = 0; i < frames; ++i) rt.render_into(sc.objects, sc.lights, {}, sc.camera, frame_buffer);
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             mismatched += frame_buffer != want;
+            const rrte_stats lst = rt.stats();
+            std::printf("engine_loop_last_frame upload_ms %.4f jit %u frames %llu\n", lst.upload_ms, lst.jit_active,
+                        (unsigned long long)lst.frames);
             out.write(reinterpret_cast<const char*>(frame_buffer.data()), (std::streamsize)frame_buffer.size());
             // of which: lowering the scene objects to the IR each frame (LoweredScene, host only)
             const auto l0 = std::chrono::steady_clock::now();
