@@ -1303,7 +1303,10 @@ JitKernel* jit_lookup(rrte_ctx* c, const std::string& key, bool topo, int mode, 
         if (pend->second.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return nullptr;
         const JitCode jc = pend->second.get();
         c->jit_pending.erase(pend);
-        if (hipSetDevice(c->device) != hipSuccess || !jit_load(jc, jk, log)) {
+        trace_rec(c, "jit: module load begin", nullptr, nullptr, (uint32_t)jc.code.size());
+        const bool loaded = hipSetDevice(c->device) == hipSuccess && jit_load(jc, jk, log);
+        trace_rec(c, "jit: module load end", nullptr, nullptr, loaded);
+        if (!loaded) {
             c->jit_log = log;
             jk = JitKernel{};
         } else {

@@ -1,6 +1,7 @@
 """The C-ABI boundary (include/rrte_hip.h): the library loads, exports every declared
 entry point, struct layouts match, and host-side argument checks work without a GPU."""
 import ctypes as C
+import os
 import re
 from pathlib import Path
 
@@ -161,3 +162,21 @@ def test_band_layout_of_the_showcase():
                                     C.byref(pb)) == abi.RRTE_INVALID_ARG
     for bad in [(0, 9, 1), (0, 1, 0), (0, 1, 9), (0, 0, 1)]:  # outside the documented ranges
         assert lib.rrte_hip_band_rows_for_rank_ex(1080, 16, 8, 1, *bad) == 0
+
+
+def test_jit_compile_writes_nothing_outside_its_temporary_directory(tmp_path):
+    """jit.hip rtc_compile: hiprtc writes the named headers under its own temporary directory
+    ($TMPDIR/comgr-*/include), resolving each name as a path; a name with "../" once put the API header
+    at $TMPDIR/include/rrte_hip.h, shared by every process on the machine, so concurrent compiles
+    (test workers, the ranks of a node) read each other's half-written copy and failed at random."""
+    import subprocess
+    import sys
+    code = ("import ctypes as C\nfrom rrte_amd import abi, LoweredScene, scenes\n"
+            "objs, lights, cam, cfg = scenes.SCENES['sdf-showcase'](32, 18)\n"
+            "sc = LoweredScene(objs, lights, cam)\nlog = C.create_string_buffer(1 << 16)\n"
+            "assert abi.load().rrte_hip_jit_check(sc.ref(), 1, log, len(log)) == abi.RRTE_OK, log.value[:2000]\n")
+    env = dict(os.environ, TMPDIR=str(tmp_path))
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(Path(__file__).resolve().parents[1]), env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert not (tmp_path / "include").exists()
