@@ -613,14 +613,18 @@ def main():
         rows = lib.rrte_hip_band_rows_for_rank_ex(H, args.band_rows, world, rank, sky.value, rb.value, pb.value)
     primary = W * rows * prm.samples_per_pixel * args.steps
     shadow = int(st.shadow_rays)
+    jit_ranks = int(st.jit_active != 0)  # ranks whose timed frames ran the scene-specialised kernel
+    if args.jit == "on" and not st.jit_active:
+        print(f"rank {rank}: the scene-specialised kernel is not active (JIT failed?); timed on the generic kernel",
+              file=sys.stderr)
 
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        cnt = torch.tensor([primary, shadow], dtype=torch.float64)
+        cnt = torch.tensor([primary, shadow, jit_ranks], dtype=torch.float64)
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        primary, shadow = int(cnt[0].item()), int(cnt[1].item())
+        primary, shadow, jit_ranks = int(cnt[0].item()), int(cnt[1].item()), int(cnt[2].item())
 
     # single-frame latency (enqueue -> frame complete on the device), D2H of the frame separately;
     # N > 1: each frame gathered on its own
@@ -831,6 +835,7 @@ def main():
                 "kernel": ("rrte_jit_kernel (scene-specialised, hiprtc)" if st.jit_active else
                            "rrte::ray_kernel<%s> (generic)" % ("LAMBERT_SHADOW" if args.mode == "lambert_shadow" else "REFCOMPAT")),
                 "jit_compile_ms": round(st.jit_compile_ms, 1) if st.jit_active else None,
+                "jit_active_ranks": f"{jit_ranks}/{world}",
                 "avg_launch_ms": round(avg_launch_ms, 5),
                 "bracket_median_ms": round(median_launch_ms, 5),
                 "bracket_mean_ms": round(mean_launch_ms, 5),
