@@ -379,8 +379,9 @@ rrte_status rrte_hip_jit_cache_key(const char* source, const char* headers_overr
 /* Diagnostic: with env RRTE_DEBUG bit 2 (value 4) set when the context was created, every wave
  * range-checks the indices it derives from its launch (tile-list slot, decoded tile, frame, output
  * row) before using them and ORs a code into a device check word instead of an out-of-range access
- * (1 list slot, 2 tile, 4 frame, 8 output row).  Drains the context's work, returns the word in *word
- * and clears it.  0 = no violation. */
+ * (1 list slot, 2 tile, 4 frame, 8 output row), and every scene upload checks the device copy's
+ * object kinds, SDF node ranges and CSG-guard links (16 kind, 32 node range, 64 guard link).  Drains
+ * the context's work, returns the word in *word and clears it.  0 = no violation. */
 rrte_status rrte_hip_check_word(rrte_ctx* ctx, uint64_t* word);
 
 /* ------------------------------------------------ SceneIR dump / load (repro) */

@@ -345,7 +345,7 @@ struct rrte_ctx {
     // Retire sets / re-profile intervals shortened for tests (RRTE_TEST_RECYCLE=1: a tile-list version
     // per launch, so the version pool wraps within a few frames)
     bool env_test_recycle = false;
-    bool env_fault_bad_slot = false;
+    int env_fault_bad_slot = 0;  // RRTE_FAULT_BAD_SLOT: 1 a tile-list slot, 2 an object kind (with RRTE_DEBUG bit 2)
     std::string dump_path;  // RRTE_DUMP_SCENE: every render call's scene + params into this file (scene_io.hip)  // RRTE_FAULT_BAD_SLOT=1 (tests, only with RRTE_DEBUG bit 2): slot 0 of every uploaded list names a tile outside the frame
     // band partition of the last multi-GPU frame (frame_band_map)
     struct {
@@ -824,6 +824,35 @@ uint32_t scene_features(const std::vector<DPrim>& prims, const std::vector<rrte_
     return f;
 }
 
+// RRTE_DEBUG bit 2 (diagnostics): the indices of the uploaded scene, checked on the DEVICE copy the
+// kernels read (one thread per object, on the upload stream right after the copy): check-
+// word bit 16 an object kind out of range, 32 an SDF node range outside the uploaded nodes, 64 a
+// CSG-guard link outside its program (it must name a later node of the same program).  The host
+// validated the caller's IR (validate); this catches a device copy that differs from it.
+__global__ __launch_bounds__(64) void scene_records_check(const DPrim* prims, uint32_t np, const rrte_sdf_node* nodes,
+                                                          uint32_t nn, unsigned long long* counters) {
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i >= np) return;
+    const DPrim& pr = prims[i];
+    uint32_t bad = 0u;
+    if (pr.kind > RRTE_PRIM_MESH) {
+        bad |= 16u;
+    } else if (pr.kind == RRTE_PRIM_SDF) {
+        if ((uint64_t)pr.sdf_first + pr.sdf_count > nn) {
+            bad |= 32u;
+        } else {
+            for (uint32_t k = 0; k < pr.sdf_count; ++k) {
+                const uint32_t link = nodes[pr.sdf_first + k].i[2];
+                if (link != 0u && (link - 1u <= k || link - 1u >= pr.sdf_count)) {
+                    bad |= 64u;
+                    break;
+                }
+            }
+        }
+    }
+    if (bad) atomicOr(counters + 1, (unsigned long long)bad);
+}
+
 rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, double* upload_ms) {
     const size_t bn = sizeof(rrte_sdf_node) * s->num_sdf_nodes;
     SceneKeyParts kparts;
@@ -906,7 +935,18 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         if (pt.bytes) memcpy(B.h_stage + pt.off, pt.src, pt.bytes);
     if (!c->upload_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking));
     hipStream_t us = c->upload_stream;
+    // fault injection for the check below (RRTE_FAULT_BAD_SLOT=2 with RRTE_DEBUG bit 2): object 0's
+    // kind out of range in the device copy only (kernels skip an unknown kind; the host copy stays valid)
+    if (c->env_fault_bad_slot == 2 && (c->env_debug & 4u) && !prims.empty())
+        reinterpret_cast<DPrim*>(B.h_stage + parts[0].off)->kind = 0xbadu;
     HIPCHK(c, hipMemcpyAsync(B.d_buf, B.h_stage, total, hipMemcpyHostToDevice, us));
+    if ((c->env_debug & 4u) && !prims.empty()) {
+        hipLaunchKernelGGL(scene_records_check, dim3(((uint32_t)prims.size() + 63u) / 64u), dim3(64), 0, us,
+                           reinterpret_cast<const DPrim*>(B.d_buf + parts[0].off), (uint32_t)prims.size(),
+                           reinterpret_cast<const rrte_sdf_node*>(B.d_buf + parts[3].off), (uint32_t)nodes.size(),
+                           c->d_counters);
+        HIPCHK(c, hipGetLastError());
+    }
     HIPCHK(c, hipEventRecord(B.ev_up, us));
     B.ordered.clear();
     // host time to lower the scene and enqueue its upload (the copy itself is asynchronous)
@@ -1562,7 +1602,7 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
     uint32_t* stage = tp.h_list[pick];
     for (size_t k = 0; k < n; ++k) stage[(k & 7u) * stride + (k >> 3)] = tp.slots[k];
     // fault injection for the device index check (tests): only where the check stops the wave first
-    if (c->env_fault_bad_slot && (c->env_debug & 4u) && n) stage[0] = hot_pack(0u, 0xfff0u);
+    if (c->env_fault_bad_slot == 1 && (c->env_debug & 4u) && n) stage[0] = hot_pack(0u, 0xfff0u);
     if (!tp.ev_up[pick] && hipEventCreateWithFlags(&tp.ev_up[pick], hipEventDisableTiming) != hipSuccess) return false;
     if (hipMemcpyAsync(tp.d_list[pick], stage, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
         hipEventRecord(tp.ev_up[pick], tp.upload_stream) != hipSuccess)
@@ -2019,7 +2059,7 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         c->env_tile_order_fixed = g[0] == '2';  // 0 image order, 2 fixed permutation (tests), else measured (default)
     }
     if (const char* g = getenv("RRTE_TEST_RECYCLE")) c->env_test_recycle = g[0] == '1';
-    if (const char* g = getenv("RRTE_FAULT_BAD_SLOT")) c->env_fault_bad_slot = g[0] == '1';
+    if (const char* g = getenv("RRTE_FAULT_BAD_SLOT")) c->env_fault_bad_slot = (g[0] == '1' || g[0] == '2') ? g[0] - '0' : 0;
     if (const char* g = getenv("RRTE_DUMP_SCENE"); g && *g) c->dump_path = g;
     if (const char* g = getenv("RRTE_BND_CHUNKS"); g && *g)
         c->bnd_chunks = std::max(1, std::min(rrte_ctx::kBndChunksMax, (int)strtol(g, nullptr, 0)));

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 
 import scenes_extra as se
-from rrte_amd import LoweredScene, abi
+from rrte_amd import LoweredScene, abi, scenes
 from rrte_amd.renderer import Context
 
 pytestmark = pytest.mark.gpu
@@ -108,3 +108,32 @@ def test_check_word_reports_a_bad_slot(monkeypatch):
         assert _check_word(ctx) == 2
         assert _check_word(ctx) == 0
         ctx.close()
+
+
+def test_check_word_reports_a_bad_scene_record(monkeypatch):
+    """The device check of the uploaded scene (rrte_hip.hip scene_records_check, RRTE_DEBUG bit 2):
+    the uploaded objects' kinds, SDF node ranges and CSG-guard links are checked on the device copy the
+    kernels read.  Clean uploads of SDF scenes with guards read 0; RRTE_FAULT_BAD_SLOT=2 puts an
+    out-of-range kind into object 0 of the device copy only, which must report code 16 (the kernels skip
+    an unknown kind, so the frame still completes)."""
+    monkeypatch.setenv("RRTE_DEBUG", "4")
+    out8 = None
+    for name in ("sdf-showcase", "deformation-stress"):
+        objs, lights, cam, cfg = scenes.SCENES[name](96, 54)
+        sc = LoweredScene(objs, lights, cam)
+        prm = cfg.lower()
+        out8 = np.empty(96 * 54 * 4, np.uint8)
+        ctx = Context(0, jit=abi.JIT_OFF)
+        ctx.check(ctx.lib.rrte_hip_render(ctx.h, sc.ref(), C.byref(prm), out8.ctypes.data))
+        assert _check_word(ctx) == 0, name
+        ctx.close()
+    objs, lights, cam, cfg = se.convex_sdf_scene(97, 61)
+    sc = LoweredScene(objs, lights, cam)
+    prm = cfg.lower()
+    out8 = np.empty(97 * 61 * 4, np.uint8)
+    monkeypatch.setenv("RRTE_FAULT_BAD_SLOT", "2")
+    ctx = Context(0, jit=abi.JIT_OFF)
+    ctx.check(ctx.lib.rrte_hip_render(ctx.h, sc.ref(), C.byref(prm), out8.ctypes.data))
+    assert _check_word(ctx) == 16
+    assert _check_word(ctx) == 0
+    ctx.close()
