@@ -97,7 +97,7 @@ struct rrte_ctx {
     static constexpr int kSceneVersions = 4;
     SceneBuf sb[kSceneVersions];
     int sb_cur = -1;
-    hipStream_t upload_stream = nullptr;  // scene H2D copies (never queued behind frames or gathers)
+    hipStream_t upload_stream = nullptr;  // scene and tile-list H2D copies (never queued behind frames or gathers)
     DPrim* d_prims = nullptr;
     DMaterial* d_mats = nullptr;
     DLight* d_lights = nullptr;
@@ -306,11 +306,12 @@ struct rrte_ctx {
         Retire ret[kVersions];
         hipEvent_t ev_up[kVersions] = {};                 // the version's upload copy done
         std::vector<hipStream_t> ordered[kVersions];     // streams already made to wait for ev_up
-        // pinned staging, one per version: a version's staging is rewritten only when the version is
-        // reused, i.e. after every launch that read it -- each of which waited for its copy (ev_up)
-        uint32_t* h_list[kVersions] = {};
-        size_t cap_h_list[kVersions] = {};
-        hipStream_t upload_stream = nullptr;
+        // pinned staging, one slice of `arena_words` per version in ONE page-locked allocation (one
+        // hipHostMalloc per growth, not one per version): a version's slice is rewritten only when the
+        // version is reused, i.e. after every launch that read it -- each of which waited for its copy
+        // (ev_up); the arena grows only when no copy out of it is pending
+        uint32_t* h_arena = nullptr;
+        size_t arena_words = 0;
         int cur = -1;                    // version holding `slots` (-1: not uploaded)
         uint64_t launches = 0;           // launches of `key` since its last profile
         uint64_t profiles = 0;           // completed profiles
@@ -933,8 +934,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     if (!B.ev_up) HIPCHK(c, hipEventCreateWithFlags(&B.ev_up, hipEventDisableTiming));
     for (const Part& pt : parts)
         if (pt.bytes) memcpy(B.h_stage + pt.off, pt.src, pt.bytes);
-    if (!c->upload_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking));
-    hipStream_t us = c->upload_stream;
+    hipStream_t us = c->upload_stream;  // (created with the context)
     // fault injection for the check below (RRTE_FAULT_BAD_SLOT=2 with RRTE_DEBUG bit 2): object 0's
     // kind out of range in the device copy only (kernels skip an unknown kind; the host copy stays valid)
     if (c->env_fault_bad_slot == 2 && (c->env_debug & 4u) && !prims.empty())
@@ -1545,23 +1545,24 @@ std::vector<uint32_t> fixed_slots(uint32_t n, uint32_t tiles_x) {
 // Words per XCD of a tile list of n slots stored XCD-major (KParams::hot_stride).
 uint32_t hot_stride(uint32_t n) { return (n + 7u) / 8u; }
 
-// Allocates what an upload of up to `words` list words needs -- pinned staging, the upload stream and
-// the device versions not yet allocated -- at profile time, so the first upload (inside a later render
-// call) allocates nothing.
+// Allocates what an upload of up to `words` list words needs -- the pinned staging arena and the device
+// versions not yet allocated -- at profile time, so the first upload (inside a later render call)
+// allocates nothing.  The copies run on the context's upload stream, created with the context: a
+// stream's first use sets up its hardware queue (~8 ms measured, profiles/r06_engine_loop_trace.log),
+// which must not land in a frame.  false = not now (a copy out of the arena is still pending).
 bool reserve_hot_lists(rrte_ctx::TileProfile& tp, size_t words) {
-    for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i)
-        if (tp.cap_h_list[i] < words && i != tp.cur) {
-            // (a version other than the current one: every launch that read it -- and its copy -- is
-            // done before it is reused; the current version's staging grows at its next reuse)
-            if (!retired_done(tp.ret[i])) continue;
-            if (tp.h_list[i]) (void)hipHostFree(tp.h_list[i]);
-            tp.h_list[i] = nullptr;
-            tp.cap_h_list[i] = 0;
-            if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_list[i]), words * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
-                return false;
-            tp.cap_h_list[i] = words;
-        }
-    if (!tp.upload_stream && hipStreamCreateWithFlags(&tp.upload_stream, hipStreamNonBlocking) != hipSuccess) return false;
+    constexpr int K = rrte_ctx::TileProfile::kVersions;
+    if (tp.arena_words < words) {
+        for (int i = 0; i < K; ++i)
+            if (tp.ev_up[i] && hipEventQuery(tp.ev_up[i]) != hipSuccess) return false;
+        if (tp.h_arena) (void)hipHostFree(tp.h_arena);
+        tp.h_arena = nullptr;
+        tp.arena_words = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&tp.h_arena), K * words * sizeof(uint32_t), hipHostMallocDefault) !=
+            hipSuccess)
+            return false;
+        tp.arena_words = words;
+    }
     for (int i = 0; i < rrte_ctx::TileProfile::kVersions; ++i)
         if (!tp.d_list[i]) {
             if (hipMalloc(reinterpret_cast<void**>(&tp.d_list[i]), words * sizeof(uint32_t)) != hipSuccess) return false;
@@ -1598,15 +1599,16 @@ bool upload_hot_list(rrte_ctx* c, rrte_ctx::TileProfile& tp) {
     trace_rec(c, "hot-list upload: device buffer", nullptr, nullptr, (uint32_t)pick);
     if (!reserve_hot_lists(tp, words)) return false;
     trace_rec(c, "hot-list upload: reserved", nullptr, nullptr, (uint32_t)pick);
-    if (tp.cap_h_list[pick] < words) return false;  // (reserve_hot_lists could not grow it yet)
-    uint32_t* stage = tp.h_list[pick];
+    uint32_t* stage = tp.h_arena + (size_t)pick * tp.arena_words;
     for (size_t k = 0; k < n; ++k) stage[(k & 7u) * stride + (k >> 3)] = tp.slots[k];
     // fault injection for the device index check (tests): only where the check stops the wave first
     if (c->env_fault_bad_slot == 1 && (c->env_debug & 4u) && n) stage[0] = hot_pack(0u, 0xfff0u);
     if (!tp.ev_up[pick] && hipEventCreateWithFlags(&tp.ev_up[pick], hipEventDisableTiming) != hipSuccess) return false;
-    if (hipMemcpyAsync(tp.d_list[pick], stage, bytes, hipMemcpyHostToDevice, tp.upload_stream) != hipSuccess ||
-        hipEventRecord(tp.ev_up[pick], tp.upload_stream) != hipSuccess)
+    trace_rec(c, "hot-list upload: staged", nullptr, nullptr, (uint32_t)pick);
+    if (hipMemcpyAsync(tp.d_list[pick], stage, bytes, hipMemcpyHostToDevice, c->upload_stream) != hipSuccess)
         return false;
+    trace_rec(c, "hot-list upload: copy queued", c->upload_stream, nullptr, (uint32_t)bytes);
+    if (hipEventRecord(tp.ev_up[pick], c->upload_stream) != hipSuccess) return false;
     tp.ordered[pick].clear();
     if (tp.cur >= 0 && retire(c, tp.ret[tp.cur]) != RRTE_OK) return false;
     tp.cur = pick;
@@ -2095,6 +2097,23 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     for (hipEvent_t& ev : c->ev_ctr)
         if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bail(e);
     if ((e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) != hipSuccess) return bail(e);
+    // the upload stream, and a first copy of a tile list's size class through it: the runtime sets up
+    // what such a copy needs at its first use (7-8 ms measured, inside the first frame of a new launch
+    // shape: profiles/r06_engine_loop_trace.log) -- here rather than in a frame
+    if ((e = hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking)) != hipSuccess) return bail(e);
+    {
+        constexpr size_t kWarm = 129600;  // a 1080p frame's list (32400 slots)
+        void *hw = nullptr, *dw = nullptr;
+        if ((e = hipHostMalloc(&hw, kWarm, hipHostMallocDefault)) != hipSuccess) return bail(e);
+        memset(hw, 0, kWarm);
+        if ((e = hipMalloc(&dw, kWarm)) == hipSuccess) {
+            e = hipMemcpyAsync(dw, hw, kWarm, hipMemcpyHostToDevice, c->upload_stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->upload_stream);
+            (void)hipFree(dw);
+        }
+        (void)hipHostFree(hw);
+        if (e != hipSuccess) return bail(e);
+    }
     if (c->fault_stall_at) {
         if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_stall), 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return bail(e);
@@ -2156,11 +2175,9 @@ void rrte_hip_destroy(rrte_ctx* c) {
             if (tp.d_list[i]) (void)hipFree(tp.d_list[i]);
             destroy_events(tp.ret[i]);
         }
-        for (uint32_t* h : tp.h_list)
-            if (h) (void)hipHostFree(h);
+        if (tp.h_arena) (void)hipHostFree(tp.h_arena);
         for (hipEvent_t e : tp.ev_up)
             if (e) (void)hipEventDestroy(e);
-        if (tp.upload_stream) (void)hipStreamDestroy(tp.upload_stream);
     }
     for (int i = 0; i < rrte_ctx::kBndChunksMax; ++i) {
         if (c->bnd_stream[i]) (void)hipStreamDestroy(c->bnd_stream[i]);
