@@ -1850,6 +1850,7 @@ rrte_status finish_frame(rrte_ctx* c, bool deferred = false) {
     HIPCHK(c, hipEventRecord(c->ev_ctr[slot], c->stream));
     rrte_status r = deferred ? spin_wait(c, c->ev_done) : RRTE_OK;
     if (r != RRTE_OK) return r;
+    trace_rec(c, "frame complete (host)", c->stream, nullptr);
     if (!deferred) HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->ctr_pending) {
         // (complete: it precedes this frame on the stream) the previous frame's counts, never read,
@@ -2214,6 +2215,7 @@ const char* rrte_hip_last_error(const rrte_ctx* c) { return c ? c->err.c_str() :
 rrte_status rrte_hip_render(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params* p, uint8_t* out) {
     if (!c) return RRTE_INVALID_ARG;
     if (!out) return fail(c, RRTE_INVALID_ARG, "null output buffer");
+    trace_rec(c, "render: enter", nullptr, nullptr);
     return render_common(c, s, p, out, nullptr);
 }
 
