@@ -271,7 +271,9 @@ struct rrte_ctx {
     bool host_prof = false;
     uint32_t env_diag_skip = 0;  // RRTE_DIAG_SKIP (1-rank timing diagnostics only): 1 no ncclGather, 2 no
                                  // de-interleave, 4 no comm-stream waits -- results are wrong
-    double hp[10] = {};
+    double hp[16] = {};  // [0, 9): gather frames; [10, 15): asynchronous frames (rrte_hip_render_async)
+    uint64_t hpa_frames = 0;
+    bool hpa_cur = false;  // inside rrte_hip_render_async (its sections go to hp[10..15))
     uint64_t hp_frames = 0;
     // RRTE_TRACE=1 (diagnostics): every event record / stream wait / launch of the frame paths with its
     // stream and event, host-timestamped, printed to stderr by rrte_hip_destroy (matched against a
@@ -1743,6 +1745,7 @@ void launch_generic(uint32_t need, dim3 grid, dim3 block, hipStream_t st, const 
 // Launch plan `L` (L.k.nframes frames) on `st`; the cached scene is the plan's.
 rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d_f32, hipStream_t st) {
     if (L.gy == 0) return RRTE_OK;
+    HostSection hsa(c);
     Cull cl{L.cull ? c->d_bounds : nullptr, L.num_prims};
     JitKernel* jk = jit_kernel_for(c, L.mode, L.cull, L.single);
     c->stats.jit_active = jk ? (jk->topology ? 2u : 1u) : 0u;
@@ -1770,13 +1773,14 @@ rrte_status issue_launch(rrte_ctx* c, LaunchPlan& L, uint32_t* d_rgba, float4* d
         MeshView mv = c->mesh_view;
         SceneValues vals{c->d_prims, c->d_mats, c->d_lights, c->d_nodes};  // read by topology kernels
         void* args[] = {&L.k, &cl, &mv, &d_rgba, &d_f32, &ctr, &vals};
+        if (c->hpa_cur) hsa.lap(13);
         HostSection hs(c);
         if (c->env_wg256)
             HIPCHK(c, hipModuleLaunchKernel(jk->fn, (L.k.width + 15) / 16, (L.k.rows + 15) / 16, L.k.nframes, 256, 1, 1,
                                             0, st, args, nullptr));
         else
             HIPCHK(c, hipModuleLaunchKernel(jk->fn, grid.x, grid.y, grid.z, kBlockThreads, 1, 1, 0, st, args, nullptr));
-        hs.lap(8);
+        hs.lap(c->hpa_cur ? 14 : 8);
         return finish_tile_order(c, L, profile, st);
     }
     SceneView sv{c->d_prims, c->d_mats, c->d_lights, c->d_nodes, L.num_prims, L.num_lights, L.num_materials,
@@ -1800,7 +1804,9 @@ rrte_status launch(rrte_ctx* c, const rrte_scene_ir* s, const rrte_render_params
                    uint32_t* d_rgba, float4* d_f32, hipStream_t st, uint32_t internal_flags = 0u, uint32_t row0 = 0u,
                    int prof = 0, const BandMap* bm = nullptr) {
     if (rows == 0) return RRTE_OK;
+    HostSection hs(c);
     LaunchPlan L = plan_launch(c, s, p, rows, internal_flags, row0, bm);
+    if (c->hpa_cur) hs.lap(12);
     L.prof = prof;
     return issue_launch(c, L, d_rgba, d_f32, st);
 }
@@ -2133,6 +2139,12 @@ void rrte_hip_destroy(rrte_ctx* c) {
         for (int i = 0; i < 9; ++i) fprintf(stderr, " %s %.2f", names[i], c->hp[i] / (double)c->hp_frames);
         fprintf(stderr, "\n");
     }
+    if (c->host_prof && c->hpa_frames) {
+        static const char* names[5] = {"validate", "scene_check", "plan", "tile_order+jit", "launch_call"};
+        fprintf(stderr, "rrte host profile (%llu async frames, us/frame):", (unsigned long long)c->hpa_frames);
+        for (int i = 0; i < 5; ++i) fprintf(stderr, " %s %.2f", names[i], c->hp[10 + i] / (double)c->hpa_frames);
+        fprintf(stderr, "\n");
+    }
     if (c->trace) {
         for (const auto& t : c->trace_log)
             fprintf(stderr, "rrte trace %12.1f us  %-34s stream %p event %p  %u %u\n", t.us, t.what, t.st, t.ev, t.a, t.b);
@@ -2229,11 +2241,15 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
                                   void* d_f32, void* stream) {
     if (!c) return RRTE_INVALID_ARG;
     dump_if_asked(c, s, p);
+    HostSection hs(c);
     rrte_status r = validate(c, s, p);
     if (r != RRTE_OK) return r;
+    hs.lap(10);
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
     double up = 0.0;
     if ((r = upload_scene(c, s, st, &up)) != RRTE_OK) return r;
+    hs.lap(11);
+    c->hpa_cur = true;
     const int nr = c->nranks, rk = c->rank;
     uint32_t rows = p->height;
     rrte_render_params pe = *p;
@@ -2248,9 +2264,11 @@ rrte_status rrte_hip_render_async(rrte_ctx* c, const rrte_scene_ir* s, const rrt
         c->rank = 0;
     }
     r = launch(c, s, &pe, rows, static_cast<uint32_t*>(d_rgba), static_cast<float4*>(d_f32), st, 0u, 0u, 0, &bm);
+    c->hpa_cur = false;
     c->nranks = nr;
     c->rank = rk;
     if (r != RRTE_OK) return r;
+    c->hpa_frames += c->host_prof;
     c->pending_primary = (uint64_t)p->width * rows * p->samples_per_pixel;
     c->stats.upload_ms = up;
     c->stats.frames++;
