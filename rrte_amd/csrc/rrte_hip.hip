@@ -108,6 +108,7 @@ struct rrte_ctx {
     // the next point where the context is idle (rrte_hip_synchronize, rrte_hip_destroy) instead of by a
     // hipFree that could wait on the device
     std::vector<void*> graveyard;
+    void *h_warm = nullptr, *d_warm = nullptr;  // the upload stream's warm-up copy (rrte_hip_create)
     Retire launched;                 // every stream that launched a frame since the last synchronisation
     uint32_t n_prims = 0, n_mats = 0, n_lights = 0, n_nodes = 0;
     // frame buffers for the blocking entry points
@@ -2110,16 +2111,13 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if ((e = hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking)) != hipSuccess) return bail(e);
     {
         constexpr size_t kWarm = 129600;  // a 1080p frame's list (32400 slots)
-        void *hw = nullptr, *dw = nullptr;
-        if ((e = hipHostMalloc(&hw, kWarm, hipHostMallocDefault)) != hipSuccess) return bail(e);
-        memset(hw, 0, kWarm);
-        if ((e = hipMalloc(&dw, kWarm)) == hipSuccess) {
-            e = hipMemcpyAsync(dw, hw, kWarm, hipMemcpyHostToDevice, c->upload_stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->upload_stream);
-            (void)hipFree(dw);
-        }
-        (void)hipHostFree(hw);
-        if (e != hipSuccess) return bail(e);
+        // (the buffers are freed with the context: a free here could wait for other contexts' frames)
+        if ((e = hipHostMalloc(&c->h_warm, kWarm, hipHostMallocDefault)) != hipSuccess) return bail(e);
+        memset(c->h_warm, 0, kWarm);
+        if ((e = hipMalloc(&c->d_warm, kWarm)) != hipSuccess ||
+            (e = hipMemcpyAsync(c->d_warm, c->h_warm, kWarm, hipMemcpyHostToDevice, c->upload_stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(c->upload_stream)) != hipSuccess)
+            return bail(e);
     }
     if (c->fault_stall_at) {
         if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_stall), 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
@@ -2175,6 +2173,8 @@ void rrte_hip_destroy(rrte_ctx* c) {
         if (b) (void)hipFree(b);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_counters2) (void)hipHostFree(c->h_counters2);
+    if (c->h_warm) (void)hipHostFree(c->h_warm);
+    if (c->d_warm) (void)hipFree(c->d_warm);
     for (hipEvent_t e : c->ev_ctr)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
