@@ -395,6 +395,7 @@ def config_leg(name, W, H, mode, dev, cpu_budget_s, flight=4, target_s=0.5):
     t0 = time.perf_counter()
     for i in range(n):
         go(i)
+    t_enq = time.perf_counter()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     c.check(lib.rrte_hip_synchronize(c.h))
@@ -423,7 +424,11 @@ def config_leg(name, W, H, mode, dev, cpu_budget_s, flight=4, target_s=0.5):
     wl = f"{name}@{W}x{H}/{mode}"
     pmc, pmc_note = pmc_traffic(wl, abi.build_id())
     leg = {"workload": None, "value": round(value, 3), "unit": "Mray/s", "ms_per_frame": round(elapsed / n * 1e3, 5),
-           "frames": n, "frames_in_flight": flight, "primary_rays_per_frame": W * H * prm.samples_per_pixel,
+           "frames": n, "frames_in_flight": flight,
+           # host time of the issue loop alone: close to ms_per_frame = the frame rate is the call rate
+           # (small frames: DESIGN.md §14 #2, tools/enqueue_rate.py)
+           "enqueue_ms_per_frame": round((t_enq - t0) / n * 1e3, 5),
+           "primary_rays_per_frame": W * H * prm.samples_per_pixel,
            "shadow_rays_per_frame": shadow / n, "kernel": "rrte_jit_kernel (scene-specialised)" if jit_active else
            "generic", "avg_launch_ms": round(launch_ms, 5),
            "roofline": {"bound": "valu", "achieved": round(valu_tf, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
