@@ -350,7 +350,7 @@ struct rrte_ctx {
     // per launch, so the version pool wraps within a few frames)
     bool env_test_recycle = false;
     int env_fault_bad_slot = 0;  // RRTE_FAULT_BAD_SLOT: 1 a tile-list slot, 2 an object kind (with RRTE_DEBUG bit 2)
-    std::string dump_path;  // RRTE_DUMP_SCENE: every render call's scene + params into this file (scene_io.hip)  // RRTE_FAULT_BAD_SLOT=1 (tests, only with RRTE_DEBUG bit 2): slot 0 of every uploaded list names a tile outside the frame
+    std::string dump_path;  // RRTE_DUMP_SCENE: every render call's scene + params into this file (scene_io.hip)
     // band partition of the last multi-GPU frame (frame_band_map)
     struct {
         bool valid = false;
