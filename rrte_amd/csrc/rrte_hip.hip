@@ -2097,7 +2097,10 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail(e);
     if ((e = hipEventCreate(&c->ev2)) != hipSuccess) return bail(e);
     if ((e = hipMalloc(reinterpret_cast<void**>(&c->d_counters), kCounterBytes)) != hipSuccess) return bail(e);
-    if ((e = hipMemset(c->d_counters, 0, kCounterBytes)) != hipSuccess) return bail(e);
+    // (on the context's stream: its first operation sets up its hardware queue, here and not in a frame)
+    if ((e = hipMemsetAsync(c->d_counters, 0, kCounterBytes, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return bail(e);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_counters), kCounterBytes, hipHostMallocDefault)) != hipSuccess) return bail(e);
     memset(c->h_counters, 0, kCounterBytes);
     if ((e = hipHostMalloc(reinterpret_cast<void**>(&c->h_counters2), kCounterBytes, hipHostMallocDefault)) != hipSuccess) return bail(e);
@@ -2109,6 +2112,13 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
     // what such a copy needs at its first use (7-8 ms measured, inside the first frame of a new launch
     // shape: profiles/r06_engine_loop_trace.log) -- here rather than in a frame
     if ((e = hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking)) != hipSuccess) return bail(e);
+    {
+        // the library's code object (every generic kernel): the runtime loads it at a kernel's first
+        // use -- ~20 ms inside the first frame otherwise (profiles/r06_engine_loop_trace_after.log)
+        hipFuncAttributes fa;
+        if ((e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&scene_records_check))) != hipSuccess)
+            return bail(e);
+    }
     {
         constexpr size_t kWarm = 129600;  // a 1080p frame's list (32400 slots)
         // (the buffers are freed with the context: a free here could wait for other contexts' frames)
