@@ -2124,9 +2124,12 @@ rrte_status rrte_hip_create(int device, rrte_ctx** out) {
         // (the buffers are freed with the context: a free here could wait for other contexts' frames)
         if ((e = hipHostMalloc(&c->h_warm, kWarm, hipHostMallocDefault)) != hipSuccess) return bail(e);
         memset(c->h_warm, 0, kWarm);
+        // (and the way back on the context's stream: a frame's tile-profile copy is a D2H of that size)
         if ((e = hipMalloc(&c->d_warm, kWarm)) != hipSuccess ||
             (e = hipMemcpyAsync(c->d_warm, c->h_warm, kWarm, hipMemcpyHostToDevice, c->upload_stream)) != hipSuccess ||
-            (e = hipStreamSynchronize(c->upload_stream)) != hipSuccess)
+            (e = hipStreamSynchronize(c->upload_stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(c->h_warm, c->d_warm, kWarm, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(c->stream)) != hipSuccess)
             return bail(e);
     }
     if (c->fault_stall_at) {
