@@ -274,6 +274,8 @@ struct rrte_ctx {
                                  // de-interleave, 4 no comm-stream waits -- results are wrong
     double hp[16] = {};  // [0, 9): gather frames; [10, 15): asynchronous frames (rrte_hip_render_async)
     uint64_t hpa_frames = 0;
+    double hpu[9] = {};     // scene uploads (upload_scene), RRTE_HOST_PROFILE sections (names at rrte_hip_destroy)
+    uint64_t hpu_n = 0;
     bool hpa_cur = false;  // inside rrte_hip_render_async (its sections go to hp[10..15))
     uint64_t hp_frames = 0;
     // RRTE_TRACE=1 (diagnostics): every event record / stream wait / launch of the frame paths with its
@@ -877,6 +879,13 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     }
     (void)st;  // the copy runs on the context's upload stream; launches wait for its event (issue_launch)
     const auto t_up0 = std::chrono::steady_clock::now();
+    auto t_sec = t_up0;
+    auto lap_up = [&](int i) {  // (RRTE_HOST_PROFILE)
+        if (!c->host_prof) return;
+        const auto n = std::chrono::steady_clock::now();
+        c->hpu[i] += std::chrono::duration<double, std::micro>(n - t_sec).count();
+        t_sec = n;
+    };
 
     for (uint32_t k = 0; k < s->num_mesh_indices; ++k)
         if (s->mesh_indices[k] >= s->num_mesh_vertices)
@@ -886,13 +895,17 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     std::vector<DLight> lights;
     std::vector<float4> bounds;
     lower_scene(s, prims, mats, lights, &bounds);
+    lap_up(0);
     MeshData md;
     build_mesh_bvhs(s, prims.data(), md, bounds.data());
     if (md.too_deep) return fail(c, RRTE_UNSUPPORTED_PRIM, "mesh BVH deeper than the traversal stack");
+    lap_up(1);
     // SDF programs with their exact CSG early-outs (sdf_guard.hpp); the key above stays the caller's IR
     std::vector<rrte_sdf_node> nodes = decorate_scene_sdf(s, c->env_guard_leaves);
+    lap_up(2);
     JitTopo topo;
     std::string tkey = topology_of(prims, lights, nodes, topo);
+    lap_up(3);
 
     // Frames in flight keep reading the current version: retire it and upload into the next version
     // of the ring once the frames that read THAT one have completed (normally long ago: a wait here
@@ -918,6 +931,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
                      {md.tris.data(), md.tris.size() * sizeof(float4), 0},
                      {md.norms.data(), md.norms.size() * sizeof(float4), 0},
                      {md.perm.data(), md.perm.size() * sizeof(uint32_t), 0}};
+    lap_up(4);
     size_t total = 0;
     for (Part& pt : parts) {
         pt.off = total;
@@ -937,12 +951,14 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
     if (!B.ev_up) HIPCHK(c, hipEventCreateWithFlags(&B.ev_up, hipEventDisableTiming));
     for (const Part& pt : parts)
         if (pt.bytes) memcpy(B.h_stage + pt.off, pt.src, pt.bytes);
+    lap_up(5);
     hipStream_t us = c->upload_stream;  // (created with the context)
     // fault injection for the check below (RRTE_FAULT_BAD_SLOT=2 with RRTE_DEBUG bit 2): object 0's
     // kind out of range in the device copy only (kernels skip an unknown kind; the host copy stays valid)
     if (c->env_fault_bad_slot == 2 && (c->env_debug & 4u) && !prims.empty())
         reinterpret_cast<DPrim*>(B.h_stage + parts[0].off)->kind = 0xbadu;
     HIPCHK(c, hipMemcpyAsync(B.d_buf, B.h_stage, total, hipMemcpyHostToDevice, us));
+    lap_up(6);
     if ((c->env_debug & 4u) && !prims.empty()) {
         hipLaunchKernelGGL(scene_records_check, dim3(((uint32_t)prims.size() + 63u) / 64u), dim3(64), 0, us,
                            reinterpret_cast<const DPrim*>(B.d_buf + parts[0].off), (uint32_t)prims.size(),
@@ -951,6 +967,7 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(B.ev_up, us));
+    lap_up(7);
     B.ordered.clear();
     // host time to lower the scene and enqueue its upload (the copy itself is asynchronous)
     *upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_up0).count();
@@ -982,6 +999,8 @@ rrte_status upload_scene(rrte_ctx* c, const rrte_scene_ir* s, hipStream_t st, do
         if (kparts.lens[i]) memcpy(k, kparts.parts[i], kparts.lens[i]);
         k += kparts.lens[i];
     }
+    lap_up(8);
+    c->hpu_n += c->host_prof;
     return RRTE_OK;
 }
 
@@ -2154,6 +2173,13 @@ void rrte_hip_destroy(rrte_ctx* c) {
         static const char* names[5] = {"validate", "scene_check", "plan", "tile_order+jit", "launch_call"};
         fprintf(stderr, "rrte host profile (%llu async frames, us/frame):", (unsigned long long)c->hpa_frames);
         for (int i = 0; i < 5; ++i) fprintf(stderr, " %s %.2f", names[i], c->hp[10 + i] / (double)c->hpa_frames);
+        fprintf(stderr, "\n");
+    }
+    if (c->host_prof && c->hpu_n) {
+        static const char* names[9] = {"lower", "mesh_bvh", "csg_guards", "topology", "version_wait", "staging",
+                                       "copy_call", "event_record", "bookkeeping"};
+        fprintf(stderr, "rrte host profile (%llu scene uploads, us/upload):", (unsigned long long)c->hpu_n);
+        for (int i = 0; i < 9; ++i) fprintf(stderr, " %s %.2f", names[i], c->hpu[i] / (double)c->hpu_n);
         fprintf(stderr, "\n");
     }
     if (c->trace) {

@@ -25,7 +25,12 @@ ap.add_argument("--width", type=int, default=640)
 ap.add_argument("--height", type=int, default=480)
 ap.add_argument("--mode", default=None)
 ap.add_argument("--frames", type=int, default=2000)
+ap.add_argument("--animated", action="store_true",
+                help="a new scene every frame (8-frame value animation, cycled; the topology kernel), as "
+                     "bench.py's topology_animated kind")
 a = ap.parse_args()
+if a.animated:
+    os.environ["RRTE_JIT_TOPO"] = "1"  # (read at context creation)
 
 dev = torch.device("cuda", 0)
 objs, lights, cam, cfg = scenes.SCENES[a.scene](a.width, a.height)
@@ -33,6 +38,7 @@ if a.mode:
     cfg.mode = a.mode
 sc = LoweredScene(objs, lights, cam)
 prm = cfg.lower()
+frames = [scenes.animate_values(LoweredScene(objs, lights, cam), f) for f in range(8)] if a.animated else [sc]
 c = Context(0, jit=abi.JIT_ON)
 lib = c.lib
 F = 4
@@ -40,16 +46,18 @@ streams = [torch.cuda.Stream(dev) for _ in range(F)]
 sp = [C.c_void_p(s.cuda_stream) for s in streams]
 outs = [torch.empty(a.width * a.height, dtype=torch.int32, device=dev) for _ in range(F)]
 optr = [o.data_ptr() for o in outs]
-h, sref, pref = c.h, sc.ref(), C.byref(prm)
+h, pref = c.h, C.byref(prm)
+refs = [f.ref() for f in frames]
+K = len(refs)
 fn = lib.rrte_hip_render_async
 for i in range(50):
-    assert fn(h, sref, pref, optr[i % F], None, sp[i % F]) == 0
+    assert fn(h, refs[i % K], pref, optr[i % F], None, sp[i % F]) == 0
 torch.cuda.synchronize(dev)
-res = {"scene": a.scene, "width": a.width, "height": a.height, "frames": a.frames}
+res = {"scene": a.scene, "width": a.width, "height": a.height, "frames": a.frames, "animated": a.animated}
 for rep in range(2):
     t0 = time.perf_counter()
     for i in range(a.frames):
-        fn(h, sref, pref, optr[i % F], None, sp[i % F])
+        fn(h, refs[i % K], pref, optr[i % F], None, sp[i % F])
     t1 = time.perf_counter()
     torch.cuda.synchronize(dev)
     t2 = time.perf_counter()
