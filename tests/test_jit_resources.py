@@ -13,7 +13,7 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 @pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="needs hipcc")
-@pytest.mark.parametrize("scene,max_vgprs", [("sdf-showcase", 64), ("basic-demo", 64)])
+@pytest.mark.parametrize("scene,max_vgprs", [("sdf-showcase", 64), ("basic-demo", 64), ("advanced-demo", 64)])
 def test_specialised_kernel_has_no_scratch(scene, max_vgprs, tmp_path):
     r = subprocess.run(["bash", str(ROOT / "tools" / "jit_isa.sh"), scene, str(tmp_path / "k.s")],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)

@@ -13,7 +13,8 @@ lib.rrte_hip_jit_check(sc.ref(), 1, None, 0)" || exit 1
 mkdir -p $T/inc && cp $R/include/rrte_hip.h $T/inc/ && cp $R/rrte_amd/csrc/device_scene.hpp $R/rrte_amd/csrc/ray_kernels.hpp $T/
 sed -i "s#../../include/rrte_hip.h#$T/inc/rrte_hip.h#" $T/device_scene.hpp
 sed -i 's/^typedef __hip_internal.*$//' $T/jit.hip && sed -i '1i #include <hip/hip_runtime.h>' $T/jit.hip
-cd $T && /opt/rocm/bin/hipcc -std=c++17 -O1 --offload-arch=gfx950 -ffp-contract=off --cuda-device-only -S -o $OUT \
+# (the JIT's own options, jit.hip rtc_options: -O1, no contraction, the max-ILP scheduler)
+cd $T && /opt/rocm/bin/hipcc -std=c++17 -O1 --offload-arch=gfx950 -ffp-contract=off -mllvm -amdgpu-sched-strategy=max-ilp --cuda-device-only -S -o $OUT \
    -Rpass-analysis=kernel-resource-usage "$@" jit.hip 2>&1 | grep -E "(VGPRs:|SGPRs:|Scratch|Occupancy)" | sed 's/.*remark: *//' | tr '\n' ' '
 echo
 python3 - "$OUT" <<'PY'
