@@ -4,6 +4,7 @@
 #include "../../include/rrte/rrte_renderer.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -570,8 +571,11 @@ LoweredScene::LoweredScene(const Objects& objects, const Lights& lights, const C
     ir_.num_mesh_vertices = (uint32_t)mesh_vertices_.size();
     ir_.mesh_indices = mesh_indices_.data();
     ir_.num_mesh_indices = (uint32_t)mesh_indices_.size();
-    static uint64_t version = 0;
-    ir_.mesh_version = mesh_indices_.empty() ? 0 : ++version;  // arrays are immutable for this object's life
+    // arrays are immutable for this object's life; the stamp is process-wide and atomic, since scenes
+    // may be lowered on several threads and two meshes must never share a stamp (the library keys its
+    // BVH cache on it: tools/tsan.sh found the plain counter racing)
+    static std::atomic<uint64_t> version{0};
+    ir_.mesh_version = mesh_indices_.empty() ? 0 : version.fetch_add(1, std::memory_order_relaxed) + 1;
 }
 
 std::vector<uint8_t> LoweredScene::bytes() const {

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Host code on several threads under ThreadSanitizer (clang's runtime, ROCm LLVM): the CPU oracle's
+# thread pool, the C++ mirror, and the host parts of librrte_hip that a context runs on its worker
+# threads (JIT source generation + hiprtc, tile-order planning, SceneIR dump / load, cache keys).
+# Device code is compiled without instrumentation (-Xarch_host).  Builds build/tsan/tsan_driver and
+# runs it; tests/test_sanitize.py drives this script.
+set -euo pipefail
+R=$(cd "$(dirname "$0")/.." && pwd)
+B=$R/build/tsan
+mkdir -p $B
+CLANG=/opt/rocm/llvm/bin/clang
+SAN="-fsanitize=thread -fno-omit-frame-pointer -g -O1"
+HSAN="-Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer"
+cd $R/rrte_amd/csrc
+make -s jit_headers.inc
+for f in rrte_hip jit bvh sdf_guard scene_io; do
+  [ $B/$f.o -nt $f.hip ] && [ $B/$f.o -nt ray_kernels.hpp ] && [ $B/$f.o -nt device_scene.hpp ] && continue
+  /opt/rocm/bin/hipcc -std=c++17 -O1 -g --offload-arch=gfx950 -ffp-contract=off -fPIC $HSAN -I/opt/rocm/include -c $f.hip -o $B/$f.o &
+done
+$CLANG -std=c11 $SAN -ffp-contract=off -pthread -c $R/oracle/rrte_oracle.c -o $B/rrte_oracle.o &
+for f in rrte_renderer examples; do
+  $CLANG++ -std=c++17 $SAN -ffp-contract=off -I$R/include -c $R/rrte_amd/cpp/$f.cpp -o $B/$f.o &
+done
+$CLANG++ -std=c++17 $SAN -I$R/include -c $R/tests/cpp/tsan_driver.cpp -o $B/tsan_driver.o &
+wait
+$CLANG++ $SAN -o $B/tsan_driver $B/tsan_driver.o $B/rrte_renderer.o $B/examples.o $B/rrte_oracle.o \
+  $B/rrte_hip.o $B/jit.o $B/bvh.o $B/sdf_guard.o $B/scene_io.o -L/opt/rocm/lib -lamdhip64 -lrccl -lhiprtc -pthread -lm \
+  -Wl,-rpath,/opt/rocm/lib
+# halt_on_error: the first race ends the run with TSan's report and a non-zero status
+TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/tsan_driver
