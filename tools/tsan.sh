@@ -4,6 +4,9 @@
 # threads (JIT source generation + hiprtc, tile-order planning, SceneIR dump / load, cache keys).
 # Device code is compiled without instrumentation (-Xarch_host).  Builds build/tsan/tsan_driver and
 # runs it; tests/test_sanitize.py drives this script.
+# `tools/tsan.sh gpu-build` instead links tests/cpp/tsan_gpu_driver.cpp (the contexts' own worker threads
+# beside two rendering threads; needs a GPU) to rrte_amd/lib/tsan_gpu_driver, which travels to the GPU
+# box, and `tools/tsan.sh gpu-run` runs it there.
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 B=$R/build/tsan
@@ -11,6 +14,11 @@ mkdir -p $B
 CLANG=/opt/rocm/llvm/bin/clang
 SAN="-fsanitize=thread -fno-omit-frame-pointer -g -O1"
 HSAN="-Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer"
+if [ "${1:-}" = gpu-run ]; then
+  RRTE_JIT_CACHE=0 RRTE_TEST_RECYCLE=1 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" \
+    timeout -k 10 300 $R/rrte_amd/lib/tsan_gpu_driver "${2:-160}"
+  exit $?
+fi
 cd $R/rrte_amd/csrc
 make -s jit_headers.inc
 for f in rrte_hip jit bvh sdf_guard scene_io; do
@@ -22,7 +30,14 @@ for f in rrte_renderer examples; do
   $CLANG++ -std=c++17 $SAN -ffp-contract=off -I$R/include -c $R/rrte_amd/cpp/$f.cpp -o $B/$f.o &
 done
 $CLANG++ -std=c++17 $SAN -I$R/include -c $R/tests/cpp/tsan_driver.cpp -o $B/tsan_driver.o &
+$CLANG++ -std=c++17 $SAN -I$R/include -c $R/tests/cpp/tsan_gpu_driver.cpp -o $B/tsan_gpu_driver.o &
 wait
+if [ "${1:-}" = gpu-build ]; then
+  $CLANG++ $SAN -o $R/rrte_amd/lib/tsan_gpu_driver $B/tsan_gpu_driver.o $B/rrte_renderer.o $B/examples.o \
+    $B/rrte_hip.o $B/jit.o $B/bvh.o $B/sdf_guard.o $B/scene_io.o -L/opt/rocm/lib -lamdhip64 -lrccl -lhiprtc -pthread -lm \
+    -Wl,-rpath,/opt/rocm/lib
+  exit 0
+fi
 $CLANG++ $SAN -o $B/tsan_driver $B/tsan_driver.o $B/rrte_renderer.o $B/examples.o $B/rrte_oracle.o \
   $B/rrte_hip.o $B/jit.o $B/bvh.o $B/sdf_guard.o $B/scene_io.o -L/opt/rocm/lib -lamdhip64 -lrccl -lhiprtc -pthread -lm \
   -Wl,-rpath,/opt/rocm/lib
