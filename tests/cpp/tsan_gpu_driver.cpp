@@ -8,6 +8,7 @@
 // generic and the specialised kernels are bit-identical).  Exits non-zero on a mismatch or an error;
 // TSan reports races on stderr.
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,8 +64,26 @@ static void worker(int id, Job a, Job b, int frames) {
         else CHECK(out == ref[k], "thread %d frame %d (%s): differs from the scene's first frame (jit %u)", id, f,
                    j.name.c_str(), s.jit_active);
     }
+    // then scene A alone until the background compile lands and the context switches kernels (the
+    // adoption path: the worker's future collected, the module loaded), bounded by time, and 16 frames past it
+    int extra = 0, after = -1;
+    const auto t0 = std::chrono::steady_clock::now();
+    out.assign((size_t)a.w * a.h * 4, 0);
+    while (after < 16 && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60)) {
+        if (rrte_hip_render(ctx, &la.ir(), &pa, out.data()) != RRTE_OK) {
+            CHECK(false, "thread %d: render (%s)", id, rrte_hip_last_error(ctx));
+            break;
+        }
+        rrte_stats s{};
+        CHECK(rrte_hip_stats(ctx, &s) == RRTE_OK, "stats");
+        jit_seen |= 1u << s.jit_active;
+        CHECK(out == ref[0], "thread %d: frame %d of the settled scene differs (jit %u)", id, extra, s.jit_active);
+        ++extra;
+        if (s.jit_active != 0 || after >= 0) ++after;
+    }
+    CHECK(after >= 16, "thread %d: the specialised kernel never became active", id);
     CHECK(rrte_hip_synchronize(ctx) == RRTE_OK, "synchronize");
-    std::printf("thread %d: %d frames, kernels seen (bit per jit kind) 0x%x\n", id, frames, jit_seen);
+    std::printf("thread %d: %d + %d frames, kernels seen (bit per jit kind) 0x%x\n", id, frames, extra, jit_seen);
     rrte_hip_destroy(ctx);
 }
 
